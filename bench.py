@@ -1,0 +1,233 @@
+"""North-star benchmark: FQL grad-steps/sec (whole node) over a 16-alpha population,
+cube-single-play shapes (BASELINE.json config 2).
+
+One "step" = one population update: every member samples its own minibatch on
+device from the HBM-resident offline buffer and runs a full FQL ``update()``
+(critic TD loss, BC flow-matching loss, 10-step Euler flow, one-step
+distillation + Q loss, backward, Adam, target EMA).  ``value`` = member
+grad-steps per second over all ranks (weak scaling: 16 members per GPU).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  Data is synthetic (no network): 1M transitions,
+obs ~ N(0,1), act ~ U(-1+1e-5, 1-1e-5), next_obs = obs + 0.05 N(0,1),
+reward in {-1, 0} with P(0) = 0.05, mask = 1 - (reward == 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "flow-q-learning_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+MI355X_FP32_MFMA_PEAK_TFLOPS = 157.3  # /opt/skills/guides/MI355X_MICROARCH.md (f32 matrix = vector peak)
+
+WORKLOADS = {
+    "cube": dict(env="cube-single-play-singletask-task2-v0", obs_dim=28, action_dim=5, batch_size=256),
+    "antsoccer": dict(env="antsoccer-arena-navigate-singletask-task4-v0", obs_dim=42, action_dim=8,
+                      batch_size=1024),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def synthetic_dataset(n_rows: int, obs_dim: int, action_dim: int, seed: int = 0) -> dict:
+    rng = np.random.default_rng(seed)
+    obs = rng.standard_normal((n_rows, obs_dim), dtype=np.float32)
+    act = rng.uniform(-1 + 1e-5, 1 - 1e-5, (n_rows, action_dim)).astype(np.float32)
+    nxt = obs + np.float32(0.05) * rng.standard_normal((n_rows, obs_dim), dtype=np.float32)
+    rew = np.where(rng.uniform(size=n_rows) < 0.05, 0.0, -1.0).astype(np.float32)
+    mask = (1.0 - (rew == 0.0)).astype(np.float32)
+    return {"observations": obs, "actions": act, "rewards": rew, "masks": mask, "next_observations": nxt}
+
+
+def population_values(n_total: int, seed: int = 0):
+    """alpha = logspace(log10 3, log10 1000, n) and seeds = random.sample(range(10000), n)
+    after random.seed(seed), as reference tune_alpha.py:40-46."""
+    random.seed(seed)
+    alphas = np.logspace(np.log10(3), np.log10(1000), num=n_total).tolist()
+    seeds = random.sample(range(10000), n_total)
+    return alphas, seeds
+
+
+def cpu_baseline(wl: dict, data: dict, budget_s: float, threads: int) -> dict:
+    """The oracle's float32 PyTorch-CPU restatement (kind "port") of one member's
+    update on the same synthetic data, timed on this host's cores."""
+    from oracle import fql_oracle as O
+    from oracle.fql_torch import TorchFQL
+
+    torch.set_num_threads(threads)
+    cfg = O.OracleConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"], batch_size=wl["batch_size"],
+                         alpha=10.0)
+    agent = TorchFQL(cfg, O.cast_tree(O.init_params(cfg, 0), np.float32))
+    rng = np.random.default_rng(1)
+    B, A, N = cfg.batch_size, cfg.action_dim, data["observations"].shape[0]
+
+    def draw():
+        idx = rng.integers(0, N, B)
+        b = {k: torch.from_numpy(np.ascontiguousarray(v[idx])) for k, v in data.items()}
+        nz = {"z_next": torch.randn(B, A), "x0": torch.randn(B, A), "t": torch.rand(B, 1),
+              "z_d": torch.randn(B, A), "z_metric": torch.randn(B, A)}
+        return b, nz
+
+    agent.update(*draw())  # warm-up
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        agent.update(*draw())
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and steps >= 3:
+            break
+    return {"value": steps / el, "unit": "member-grad-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} sequential update() steps of 1 member (alpha=10, B={B}, H=512) in {el:.1f} s, "
+                      f"float32 PyTorch-CPU restatement (oracle/fql_torch.py), torch threads={threads}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--members", type=int, default=16, help="population members per GPU")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cube")
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-iters", type=int, default=100)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    torch.cuda.set_device(local_rank)
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from fqlpop import Population, PopulationConfig
+
+    wl = WORKLOADS[args.workload]
+    # dataset: generated on rank 0, broadcast over RCCL (xGMI) to every rank
+    data = synthetic_dataset(args.rows, wl["obs_dim"], wl["action_dim"]) if rank == 0 else None
+    keys = ("observations", "actions", "rewards", "masks", "next_observations")
+    dev = torch.device("cuda", local_rank)
+    shapes = {"observations": (args.rows, wl["obs_dim"]), "actions": (args.rows, wl["action_dim"]),
+              "rewards": (args.rows,), "masks": (args.rows,), "next_observations": (args.rows, wl["obs_dim"])}
+    dev_data = {}
+    for k in keys:
+        t = torch.from_numpy(data[k]).to(dev) if rank == 0 else torch.empty(shapes[k], dtype=torch.float32, device=dev)
+        if distributed:
+            dist.broadcast(t, src=0)
+        dev_data[k] = t
+    torch.cuda.synchronize()
+
+    alphas_all, seeds_all = population_values(args.members * world)
+    alphas, seeds = alphas_all[rank::world], seeds_all[rank::world]
+    pcfg = PopulationConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"], batch_size=wl["batch_size"],
+                            use_graph=not args.no_graph)
+    pop = Population(pcfg, alphas, seeds, device=local_rank)
+    pop.set_dataset(dev_data)
+    del dev_data
+    torch.cuda.empty_cache()
+
+    log(f"[rank {rank}] warmup {args.warmup} steps, {pop.n} members")
+    pop.step(args.warmup)
+    pop.sync()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    chunk = max(1, min(100, args.steps))
+    done = 0
+    while done < args.steps:
+        k = min(chunk, args.steps - done)
+        pop.step(k)
+        done += k
+    pop.sync()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if distributed:
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    info = pop.read_info_array()
+    finite = bool(np.all(np.isfinite(info[:, :13])))
+
+    member_steps = args.members * world * args.steps
+    value = member_steps / el
+    flops_ms = pop.flops_per_member_step
+
+    # dominant kernel: hidden-layer forward GEMM of the Euler flow (all members, one launch)
+    avg_us, kflops = pop.time_dominant_kernel(args.kernel_iters)
+    achieved = kflops / (avg_us * 1e-6) / 1e12
+
+    result = {
+        "metric": "FQL grad-steps/sec (whole node) over 16-alpha population, cube-single-v0"
+        if args.workload == "cube" else "FQL grad-steps/sec (whole node) over 16-alpha population, antsoccer",
+        "value": round(value, 2),
+        "unit": "member-grad-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * el / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (1M transitions of cube-single shape, seeded numpy; random-init weights)",
+        "config": {
+            "workload": f"{wl['env']} 16-alpha population update(), B={wl['batch_size']}, H=512x4, "
+                        f"obs {wl['obs_dim']}, act {wl['action_dim']}, flow_steps 10",
+            "members_per_gpu": args.members,
+            "global_batch": wl["batch_size"] * args.members * world,
+            "population_steps_per_s": round(args.steps / el, 3),
+            "gflop_per_member_step": round(flops_ms / 1e9, 4),
+            "step_tflops": round(flops_ms * value / 1e12, 3),
+            "step_mfma_frac": round(flops_ms * value / 1e12 / (MI355X_FP32_MFMA_PEAK_TFLOPS * world), 4),
+            "parallelism": f"weak: {args.members} members per GPU x {world} GPU(s), no data-path collective",
+            "graph": not args.no_graph,
+            "info_finite": finite,
+        },
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "gemm_kernel<fwd, bias+gelu> (Euler-flow hidden layer, 512x512 @ 512xB per member)",
+            "achieved": round(achieved, 3),
+            "peak": MI355X_FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / MI355X_FP32_MFMA_PEAK_TFLOPS, 4),
+            "avg_launch_us": round(avg_us, 3),
+            "flops_per_launch": kflops,
+            "traffic": None,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+        log(f"[rank 0] cpu baseline ({args.cpu_baseline_seconds:.0f} s budget, {threads} threads)")
+        result["cpu_baseline"] = cpu_baseline(wl, data, args.cpu_baseline_seconds, threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    pop.close()
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+// Internal interface between the HIP kernels (kernels.hip) and the host
+// runtime (runtime.cpp).  Not part of the C ABI.
+//
+// Data layout in HBM: every activation is stored
+// FEATURE-MAJOR, x'[feature][row] (row = minibatch element, contiguous), so
+// the forward Dense layer  y = x W + b  is computed as  y' = W^T x'  with both
+// MFMA operands read straight from memory (W is [in][out] row-major, the flax
+// layout).  Every per-member tensor lives at base + slot * slot_stride
+// (+ e * ens_stride for the critic ensemble).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fq {
+
+// Tensor reference: pointer + element stride per population slot and per
+// sub-batch index (critic ensemble member).
+struct TRef {
+    float* p;
+    long long ss;  // slot stride
+    long long sy;  // ensemble (y) stride
+};
+
+inline TRef tref(float* p, long long ss, long long sy = 0) { return TRef{p, ss, sy}; }
+
+// ---------------------------------------------------------------- GEMM ----
+// C[i][j] = sum_r A(i,r) B(r,j)   (fp32 in, fp32 accumulate, MFMA 32x32x2)
+//   A(i,r) = A_RC ? A[i*lda + r] : A[r*lda + i]
+//   B(r,j) = B_RC ? B[j*ldb + r] : B[r*ldb + j]
+enum GemmLayout { LAYOUT_FWD = 0, LAYOUT_DX = 1, LAYOUT_DW = 2 };
+enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU2 = 2, EPI_BIAS_GELU = 3 };
+
+struct GemmArgs {
+    TRef A, B, C, C2, bias;
+    int M, N, K;
+    int lda, ldb, ldc;
+    int ny, nz;
+    const int* slots;
+};
+// tile: 0 = 64x64, 1 = 128x64 (i x j), 2 = 64x128, 3 = 128x128
+void launch_gemm(int layout, int epi, int tile, const GemmArgs& a, hipStream_t s);
+
+// ------------------------------------------------------- row-wise kernels --
+struct LnArgs {           // h = LN(gelu(u)) * gamma + beta, per column
+    TRef u, h, mu, rstd, gamma, beta;
+    int H, M, ld;         // features, columns, leading dim (columns of buffer)
+    int ny, nz;
+    const int* slots;
+};
+void launch_ln_gelu_fwd(const LnArgs& a, hipStream_t s);
+
+enum HeadMode { HEAD_STORE = 0, HEAD_BC_FUSED = 1, HEAD_EULER = 2, HEAD_OS = 3, HEAD_ACT = 4 };
+struct HeadArgs {         // out'[j][m] = sum_k W[k][j] h'[k][m] + b[j]
+    TRef h, W, b;
+    TRef o0, o1, o2, o3;  // mode-dependent outputs (see kernels.hip)
+    int H, M, ld, nout;
+    int ld0, ld1, ld2, ld3;
+    int B, D;             // batch size, obs dim (row offsets into input buffers)
+    int last;             // HEAD_EULER: final step (write clipped actions)
+    float steps_f;        // flow_steps as float (divisor of the Euler update)
+    float t_next;         // HEAD_EULER/BC_FUSED: time row value of the next step
+    int ny, nz;
+    const int* slots;
+};
+void launch_head_fwd(int mode, const HeadArgs& a, hipStream_t s);
+
+struct BwdArgs {
+    TRef dh;              // [H][ld_d] gradient w.r.t. layer output (non-head mode)
+    TRef dout, W5;        // head mode: dout'[nout][ld_o], W5[H][nout]
+    TRef u, x_head;       // u'[H][ld] pre-activation; x_head'[H][ld] head input (LN output)
+    TRef mu, rstd, gamma; // LN
+    TRef c1, c2;          // LN row statistics of the backward pass [ld]
+    TRef du;              // [H][ld_d] output
+    TRef g_b, g_gamma, g_beta, g_W5;  // grads (written, not accumulated)
+    int H, M, Mg, ld, ld_d, ld_o, nout;
+    int ny, nz;
+    const int* slots;
+};
+void launch_bwd_rowstats(bool head, const BwdArgs& a, hipStream_t s);
+void launch_bwd_cols(bool head, bool ln, const BwdArgs& a, hipStream_t s);
+
+struct InGradArgs {       // da'[j][m] = sum_e sum_n W0_e[(D+j)][n] du0_e'[n][off+m]
+    TRef W0, du0, da;
+    int H, D, A, E, ld, off, M;
+    int nz;
+    const int* slots;
+};
+void launch_input_grad(const InGradArgs& a, hipStream_t s);
+
+// --------------------------------------------------------------- batch ----
+struct SampleArgs {
+    // dataset (row-major) or injected staging (per active member, packed)
+    const float *obs, *act, *rew, *mask, *nobs;
+    long long n_rows;
+    const float* inj_batch;   // non-null => injected mode
+    const float* inj_noise;
+    const uint64_t* seeds;    // per slot
+    const int* count;         // per slot (Adam count == update index)
+    unsigned stream_salt;     // distinguishes train / val draws
+    int B, D, A;
+    // outputs (feature-major)
+    TRef os_in;   // [D+A][3B]
+    TRef bc_in;   // [D+A+1][2B]
+    TRef cr_in;   // [D+A][2B]
+    TRef tg_in;   // [D+A][B]
+    TRef eu_in;   // [D+A+1][B]
+    TRef act_t, x0_t, rew_t, mask_t;  // [A][B], [A][B], [B], [B]
+    int nz;
+    const int* slots;
+};
+void launch_sample(const SampleArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- loss ----
+struct LossArgs {
+    TRef q, qt, rew, mask;        // q'[E][2B], qt'[E][B]
+    TRef vpred, act, x0, amet;    // [A][B]
+    TRef apiraw, aflow, da;       // [A][B]
+    TRef dq;                      // out [E][2B]
+    TRef dv;                      // out [A][B]
+    TRef dout_os;                 // out [A][B]
+    TRef g_cb4, g_bcb4, g_osb4;   // head-bias grads: critic [E] (ens stride), bc [A], os [A]
+    TRef info;                    // [16]
+    const float* alpha;           // per slot
+    int B, A, E;
+    int q_min, normq;
+    float discount;
+    int nz;
+    const int* slots;
+};
+void launch_loss_critic(const LossArgs& a, hipStream_t s);
+void launch_loss_bc(const LossArgs& a, hipStream_t s);
+void launch_loss_actor(const LossArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------- optimiser ----
+struct Chunk { long long off; int len; int leaf; };  // element offset into a net's param block
+struct AdamArgs {
+    float *p, *g, *m, *v;         // arenas (slot stride P)
+    float* target;                // target arena (slot stride PT) or null
+    long long P, PT;
+    long long net_off;            // offset of this net inside the params arena
+    const Chunk* chunks;          // chunk table of this net
+    int n_chunks, chunk_base;     // chunk ids chunk_base.. in the stats slab
+    float* stats;                 // [slots][n_total_chunks][3] (max, min, sumsq)
+    int n_total_chunks;
+    const int* count;
+    float lr, tau;
+    int nz;
+    const int* slots;
+};
+void launch_adam(const AdamArgs& a, hipStream_t s);
+
+struct FinalArgs {
+    const float* stats;           // [slots][n_total_chunks][3]
+    const int* chunk_leaf;        // leaf id of every chunk
+    int n_total_chunks, n_leaves;
+    TRef info;
+    int* count;
+    int nz;
+    const int* slots;
+};
+void launch_finalize(const FinalArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- init ----
+struct InitArgs {                 // uniform(-lim, lim) fill of one tensor of one slot
+    float* p;
+    long long n;
+    float lim;                    // 0 => constant fill with `value`
+    float value;
+    uint64_t seed;
+    unsigned salt;
+};
+void launch_init(const InitArgs& a, hipStream_t s);
+
+}  // namespace fq

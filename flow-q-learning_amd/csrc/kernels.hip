@@ -1,0 +1,1025 @@
+// HIP / CDNA4 (gfx950) kernels of the FQL population update.
+//
+// One launch of every kernel covers ALL active population members
+// (blockIdx -> (tile, ensemble member y, member z); z -> slot via `slots`).
+// Activations are feature-major x'[feature][row]; see kernels.h.
+//
+// Reference semantics ([EXT] upstream fql, restated in SURVEY.md App. A and
+// oracle/fql_oracle.py):
+//   MLP  (fql/utils/networks.py)      -> gemm_kernel + ln_gelu_fwd_kernel + head_fwd_kernel
+//   critic_loss / actor_loss (fql/agents/fql.py) -> loss_* kernels
+//   jax.grad                           -> bwd_* kernels + gemm_kernel (dX, dW layouts)
+//   optax.adam + target_update         -> adam_kernel ; apply_loss_fn grad stats -> finalize_kernel
+#include "kernels.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+namespace fq {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define DEV __device__ __forceinline__
+
+DEV float* at(TRef t, int slot, int y = 0) {
+    return t.p + (long long)slot * t.ss + (long long)y * t.sy;
+}
+
+constexpr float kSqrt2OverPi = 0.7978845608028654f;
+
+DEV float gelu_f(float x) {
+    const float y = kSqrt2OverPi * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.0f + tanhf(y));
+}
+
+DEV float gelu_grad_f(float x) {
+    const float t = tanhf(kSqrt2OverPi * (x + 0.044715f * x * x * x));
+    return 0.5f * (1.0f + t) +
+           0.5f * x * (1.0f - t * t) * kSqrt2OverPi * (1.0f + 3.0f * 0.044715f * x * x);
+}
+
+DEV float clip1(float x) { return fminf(fmaxf(x, -1.0f), 1.0f); }
+
+DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+DEV float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+DEV float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Block-wide reductions for 256-thread blocks; `red` needs 4 floats.
+DEV float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+DEV float block_max(float v, float* red) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+DEV float block_min(float v, float* red) {
+    v = wave_min(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
+}
+
+// Bijective XCD-aware remap: blocks b and b+8 share an XCD under round-robin
+// dispatch, so give each XCD a contiguous range of logical work ids (members'
+// tiles then share that XCD's L2 for their weight panel).  Speed only.
+DEV int xcd_remap(int bid, int total) {
+    const int q = total >> 3, r = total & 7, x = bid & 7, loc = bid >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
+}
+
+// =============================================================== GEMM ======
+// C[i][j] = sum_r A(i,r) B(r,j) over one (member, ensemble) pair per block
+// tile.  256 threads = 4 waves in a 2x2 grid; each wave owns (BM/2)x(BN/2)
+// built from 32x32 v_mfma_f32_32x32x2_f32 tiles (exact fp32 fma chain).
+// K staged through LDS in BK=32 slices, register double-buffered: the global
+// loads of slice k+1 are in flight while slice k feeds the MFMAs.
+// LDS images: i-contiguous operands are stored [r][i] (lanes 0..31 read 32
+// consecutive floats: conflict-free ds_read_b32); r-contiguous operands are
+// stored [i][r] with row pitch BK+1 (bank = (i + r) mod 32: conflict-free).
+
+// Global -> register staging of one operand slice.  An "IC" (i-contiguous)
+// operand slice is BK rows (r) x TILE cols (i); an "RC" slice is TILE rows (i)
+// x BK cols (r).  Element p of the thread's float4 list; rows beyond `rows`
+// or columns beyond `cols` read as zero.
+template <int TILE, int BK, bool RC>
+DEV float4 stage_load(const float* __restrict__ X, int ld, int p, int i0, int k0, int ilim, int klim) {
+    const int idx = threadIdx.x + 256 * p;
+    if constexpr (RC) {
+        const int row = idx / (BK / 4), c = (idx % (BK / 4)) * 4;
+        const int gi = i0 + row, gr = k0 + c;
+        if (gi < ilim && gr < klim) return *reinterpret_cast<const float4*>(X + (long long)gi * ld + gr);
+    } else {
+        const int row = idx / (TILE / 4), c = (idx % (TILE / 4)) * 4;
+        const int gr = k0 + row, gi = i0 + c;
+        if (gr < klim && gi < ilim) return *reinterpret_cast<const float4*>(X + (long long)gr * ld + gi);
+    }
+    return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <int TILE, int BK, bool RC>
+DEV void stage_store(float* __restrict__ S, int p, float4 v) {
+    const int idx = threadIdx.x + 256 * p;
+    if constexpr (RC) {
+        const int row = idx / (BK / 4), c = (idx % (BK / 4)) * 4;
+        float* d = S + row * (BK + 1) + c;
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    } else {
+        const int row = idx / (TILE / 4), c = (idx % (TILE / 4)) * 4;
+        *reinterpret_cast<float4*>(S + row * TILE + c) = v;
+    }
+}
+
+template <int BM, int BN, bool ARC, bool BRC, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
+    constexpr int BK = 32;
+    constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+    constexpr int A_SZ = ARC ? BM * (BK + 1) : BK * BM;
+    constexpr int B_SZ = BRC ? BN * (BK + 1) : BK * BN;
+    constexpr int A_LD = BM * BK / 1024;  // float4 loads per thread
+    constexpr int B_LD = BN * BK / 1024;
+    __shared__ __attribute__((aligned(16))) float smem[2 * (A_SZ + B_SZ)];
+
+    const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
+    const int per = tiles_m * tiles_n;
+    const int total = per * g.ny * g.nz;
+    const int w = xcd_remap(blockIdx.x, total);
+    const int tile = w % per, yz = w / per;
+    const int y = yz % g.ny, z = yz / g.ny;
+    const int slot = g.slots[z];
+    const int i0 = (tile / tiles_n) * BM, j0 = (tile % tiles_n) * BN;
+
+    const float* __restrict__ A = at(g.A, slot, y);
+    const float* __restrict__ B = at(g.B, slot, y);
+    const int tid = threadIdx.x;
+    // scalar copies: lambdas must not capture the kernarg struct by reference
+    // (that materialises it in scratch)
+    const int gM = g.M, gN = g.N, gK = g.K, lda = g.lda, ldb = g.ldb;
+
+    float4 ra[A_LD], rb[B_LD];
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wi = (wave >> 1) * WM, wj = (wave & 1) * WN;
+    const int l32 = lane & 31, lh = lane >> 5;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+    float* As0 = smem;
+    float* Bs0 = smem + A_SZ;
+    float* As1 = smem + A_SZ + B_SZ;
+    float* Bs1 = As1 + A_SZ;
+
+    const int nk = (gK + BK - 1) / BK;
+#define FQ_LOAD(k0)                                                                              \
+    _Pragma("unroll") for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, ARC>(A, lda, p, i0, k0, gM, gK); \
+    _Pragma("unroll") for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, BRC>(B, ldb, p, j0, k0, gN, gK);
+#define FQ_STORE(As, Bs)                                                                         \
+    _Pragma("unroll") for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, ARC>(As, p, ra[p]);     \
+    _Pragma("unroll") for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC>(Bs, p, rb[p]);
+    FQ_LOAD(0)
+    FQ_STORE(As0, Bs0)
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const float* Ac = (kt & 1) ? As1 : As0;
+        const float* Bc = (kt & 1) ? Bs1 : Bs0;
+        const bool more = kt + 1 < nk;
+        if (more) {
+            FQ_LOAD((kt + 1) * BK)
+        }
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; ++kk) {
+            const int rr = 2 * kk + lh;
+            float av[TM], bv[TN];
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+                av[a] = ARC ? Ac[(wi + a * 32 + l32) * (BK + 1) + rr] : Ac[rr * BM + wi + a * 32 + l32];
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+                bv[b] = BRC ? Bc[(wj + b * 32 + l32) * (BK + 1) + rr] : Bc[rr * BN + wj + b * 32 + l32];
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+        }
+        if (more) {
+            float* An = (kt & 1) ? As0 : As1;
+            float* Bn = (kt & 1) ? Bs0 : Bs1;
+            FQ_STORE(An, Bn)
+        }
+        __syncthreads();
+    }
+#undef FQ_LOAD
+#undef FQ_STORE
+
+    // epilogue: accumulator register r of a 32x32 tile holds
+    // row i = (r&3) + 8*(r>>2) + 4*(lane>>5), column j = lane&31.
+    float* __restrict__ C = at(g.C, slot, y);
+    float* __restrict__ C2 = (EPI == EPI_BIAS_GELU2) ? at(g.C2, slot, y) : nullptr;
+    const float* __restrict__ bias = (EPI != EPI_STORE) ? at(g.bias, slot, y) : nullptr;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = i0 + wi + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int j = j0 + wj + b * 32 + l32;
+                if (i < g.M && j < g.N) {
+                    float v = acc[a][b][r];
+                    const long long o = (long long)i * g.ldc + j;
+                    if constexpr (EPI == EPI_STORE) {
+                        C[o] = v;
+                    } else if constexpr (EPI == EPI_BIAS) {
+                        C[o] = v + bias[i];
+                    } else if constexpr (EPI == EPI_BIAS_GELU2) {
+                        v += bias[i];
+                        C[o] = v;
+                        C2[o] = gelu_f(v);
+                    } else {
+                        C[o] = gelu_f(v + bias[i]);
+                    }
+                }
+            }
+}
+
+template <bool ARC, bool BRC, int EPI>
+static void gemm_dispatch_tile(int tile, const GemmArgs& a, hipStream_t s) {
+    auto grid = [&](int bm, int bn) {
+        return dim3(((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) * a.ny * a.nz);
+    };
+    switch (tile) {
+        case 0: hipLaunchKernelGGL((gemm_kernel<64, 64, ARC, BRC, EPI>), grid(64, 64), dim3(256), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((gemm_kernel<128, 64, ARC, BRC, EPI>), grid(128, 64), dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((gemm_kernel<64, 128, ARC, BRC, EPI>), grid(64, 128), dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL((gemm_kernel<128, 128, ARC, BRC, EPI>), grid(128, 128), dim3(256), 0, s, a); break;
+    }
+}
+
+void launch_gemm(int layout, int epi, int tile, const GemmArgs& a, hipStream_t s) {
+    if (layout == LAYOUT_FWD) {
+        switch (epi) {
+            case EPI_BIAS: gemm_dispatch_tile<false, false, EPI_BIAS>(tile, a, s); break;
+            case EPI_BIAS_GELU2: gemm_dispatch_tile<false, false, EPI_BIAS_GELU2>(tile, a, s); break;
+            default: gemm_dispatch_tile<false, false, EPI_BIAS_GELU>(tile, a, s); break;
+        }
+    } else if (layout == LAYOUT_DX) {
+        gemm_dispatch_tile<true, false, EPI_STORE>(tile, a, s);
+    } else {
+        gemm_dispatch_tile<true, true, EPI_STORE>(tile, a, s);
+    }
+}
+
+// ======================================================= LayerNorm fwd =====
+// h'[k][m] = (gelu(u'[k][m]) - mu[m]) * rstd[m] * gamma[k] + beta[k]
+// (flax LayerNorm eps 1e-6, fast variance, after GELU).  Block = 64 columns x
+// 4 waves splitting the features; stats combined through LDS.
+__global__ __launch_bounds__(256) void ln_gelu_fwd_kernel(const LnArgs a) {
+    const int ncb = a.M / 64;
+    const int cb = blockIdx.x % ncb, yz = blockIdx.x / ncb;
+    const int y = yz % a.ny, z = yz / a.ny;
+    const int slot = a.slots[z];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int m = cb * 64 + lane;
+    const float* __restrict__ u = at(a.u, slot, y);
+    float* __restrict__ h = at(a.h, slot, y);
+    const float* __restrict__ gam = at(a.gamma, slot, y);
+    const float* __restrict__ bet = at(a.beta, slot, y);
+    const int kq = a.H / 4, k0 = w * kq;
+    float s1 = 0.f, s2 = 0.f;
+    for (int k = k0; k < k0 + kq; ++k) {
+        const float gv = gelu_f(u[(long long)k * a.ld + m]);
+        s1 += gv;
+        s2 += gv * gv;
+    }
+    __shared__ float red[2][4][64];
+    red[0][w][lane] = s1;
+    red[1][w][lane] = s2;
+    __syncthreads();
+    const float S1 = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
+    const float S2 = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+    const float mean = S1 / (float)a.H;
+    const float var = fmaxf(S2 / (float)a.H - mean * mean, 0.f);
+    const float rs = 1.0f / sqrtf(var + 1e-6f);
+    for (int k = k0; k < k0 + kq; ++k) {
+        const long long o = (long long)k * a.ld + m;
+        const float gv = gelu_f(u[o]);
+        h[o] = (gv - mean) * rs * gam[k] + bet[k];
+    }
+    if (w == 0) {
+        at(a.mu, slot, y)[m] = mean;
+        at(a.rstd, slot, y)[m] = rs;
+    }
+}
+
+void launch_ln_gelu_fwd(const LnArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(ln_gelu_fwd_kernel, dim3((a.M / 64) * a.ny * a.nz), dim3(256), 0, s, a);
+}
+
+// ============================================================ head fwd =====
+// Last Dense layer (out width 1 or action_dim <= 8): one lane per column,
+// weights are wave-uniform (scalar loads); 4 waves split the features.
+// Modes fuse what consumes the head output:
+//   HEAD_STORE    o0[j][m] = v                              (critic Q)
+//   HEAD_BC_FUSED M = 2B: m <  B -> o0 = v_theta prediction (BC loss)
+//                         m >= B -> Euler step 0: x1 = z_d + v/steps into o2
+//                         (= Euler input rows D..D+A-1), time row D+A = t_next
+//   HEAD_EULER    x += v/steps in o2 rows; last step: o0 = clip(x) (a_flow)
+//   HEAD_OS       M = 3B: [0,B) a' = clip(v) -> o1 (target-critic input rows)
+//                 [B,2B) a_pi = v -> o0, clip(a_pi) -> o2 cols B.. (critic input)
+//                 [2B,3B) clip(v) -> o3 (mse metric actions)
+//   HEAD_ACT      o0 = clip(v)                              (sample_actions)
+template <int MODE>
+__global__ __launch_bounds__(256) void head_fwd_kernel(const HeadArgs a) {
+    const int ncb = a.M / 64;
+    const int cb = blockIdx.x % ncb, yz = blockIdx.x / ncb;
+    const int y = yz % a.ny, z = yz / a.ny;
+    const int slot = a.slots[z];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m = cb * 64 + lane;
+    const float* __restrict__ h = at(a.h, slot, y);
+    const float* __restrict__ W = at(a.W, slot, y);
+    const int nout = a.nout;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    const int kq = a.H / 4, k0 = w * kq;
+    for (int k = k0; k < k0 + kq; ++k) {
+        const float hv = h[(long long)k * a.ld + m];
+        const float* wr = W + (long long)k * nout;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j < nout) acc[j] += wr[j] * hv;
+    }
+    __shared__ float red[4][8][64];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[w][j][lane] = acc[j];
+    __syncthreads();
+    if (w != 0) return;
+    const float* __restrict__ bias = at(a.b, slot, y);
+    const int B = a.B, D = a.D;
+    for (int j = 0; j < nout; ++j) {
+        const float v = (red[0][j][lane] + red[1][j][lane]) + (red[2][j][lane] + red[3][j][lane]) + bias[j];
+        if constexpr (MODE == HEAD_STORE) {
+            at(a.o0, slot, y)[(long long)j * a.ld0 + m] = v;
+        } else if constexpr (MODE == HEAD_ACT) {
+            at(a.o0, slot, y)[(long long)j * a.ld0 + m] = clip1(v);
+        } else if constexpr (MODE == HEAD_BC_FUSED) {
+            if (m < B) {
+                at(a.o0, slot)[(long long)j * a.ld0 + m] = v;
+            } else {
+                const int mm = m - B;
+                const float x = at(a.o1, slot)[(long long)(D + j) * a.ld1 + m];
+                float* eu = at(a.o2, slot);
+                eu[(long long)(D + j) * a.ld2 + mm] = x + v / a.steps_f;
+                if (j == 0) eu[(long long)(D + nout) * a.ld2 + mm] = a.t_next;
+            }
+        } else if constexpr (MODE == HEAD_EULER) {
+            float* eu = at(a.o2, slot);
+            const long long o = (long long)(D + j) * a.ld2 + m;
+            const float xn = eu[o] + v / a.steps_f;
+            if (a.last) {
+                at(a.o0, slot)[(long long)j * a.ld0 + m] = clip1(xn);
+            } else {
+                eu[o] = xn;
+                if (j == 0) eu[(long long)(D + nout) * a.ld2 + m] = a.t_next;
+            }
+        } else if constexpr (MODE == HEAD_OS) {
+            if (m < B) {
+                at(a.o1, slot)[(long long)(D + j) * a.ld1 + m] = clip1(v);
+            } else if (m < 2 * B) {
+                const int mm = m - B;
+                at(a.o0, slot)[(long long)j * a.ld0 + mm] = v;
+                at(a.o2, slot)[(long long)(D + j) * a.ld2 + B + mm] = clip1(v);
+            } else {
+                at(a.o3, slot)[(long long)j * a.ld3 + (m - 2 * B)] = clip1(v);
+            }
+        }
+    }
+}
+
+void launch_head_fwd(int mode, const HeadArgs& a, hipStream_t s) {
+    const dim3 grid((a.M / 64) * a.ny * a.nz), blk(256);
+    switch (mode) {
+        case HEAD_STORE: hipLaunchKernelGGL(head_fwd_kernel<HEAD_STORE>, grid, blk, 0, s, a); break;
+        case HEAD_BC_FUSED: hipLaunchKernelGGL(head_fwd_kernel<HEAD_BC_FUSED>, grid, blk, 0, s, a); break;
+        case HEAD_EULER: hipLaunchKernelGGL(head_fwd_kernel<HEAD_EULER>, grid, blk, 0, s, a); break;
+        case HEAD_OS: hipLaunchKernelGGL(head_fwd_kernel<HEAD_OS>, grid, blk, 0, s, a); break;
+        default: hipLaunchKernelGGL(head_fwd_kernel<HEAD_ACT>, grid, blk, 0, s, a); break;
+    }
+}
+
+// ============================================================ backward =====
+// Gradient w.r.t. a hidden layer's output, either from memory (dh') or, for
+// the last hidden layer, recomputed from the head: dh[k][m] = sum_j W5[k][j] dout[j][m].
+template <bool HEAD>
+DEV float load_dh(const float* __restrict__ dh, const float* __restrict__ W5, const float* dov,
+                  int nout, int k, int m, int ld_d) {
+    if constexpr (HEAD) {
+        float s = 0.f;
+        const float* wr = W5 + (long long)k * nout;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j < nout) s += wr[j] * dov[j];
+        return s;
+    } else {
+        return dh[(long long)k * ld_d + m];
+    }
+}
+
+// LN backward row statistics: c1[m] = mean_k(dxhat), c2[m] = mean_k(dxhat*xhat)
+// with dxhat = dh*gamma, xhat = (gelu(u)-mu)*rstd.
+template <bool HEAD>
+__global__ __launch_bounds__(256) void bwd_rowstats_kernel(const BwdArgs a) {
+    const int ncb = a.M / 64;
+    const int cb = blockIdx.x % ncb, yz = blockIdx.x / ncb;
+    const int y = yz % a.ny, z = yz / a.ny;
+    const int slot = a.slots[z];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m = cb * 64 + lane;
+    const float* __restrict__ u = at(a.u, slot, y);
+    const float* __restrict__ dh = HEAD ? nullptr : at(a.dh, slot, y);
+    const float* __restrict__ W5 = HEAD ? at(a.W5, slot, y) : nullptr;
+    const float* __restrict__ gam = at(a.gamma, slot, y);
+    const float mu = at(a.mu, slot, y)[m], rs = at(a.rstd, slot, y)[m];
+    float dov[8];
+    if constexpr (HEAD) {
+        const float* dout = at(a.dout, slot, y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dov[j] = (j < a.nout) ? dout[(long long)j * a.ld_o + m] : 0.f;
+    }
+    const int kq = a.H / 4, k0 = w * kq;
+    float s1 = 0.f, s2 = 0.f;
+    for (int k = k0; k < k0 + kq; ++k) {
+        const float dhv = load_dh<HEAD>(dh, W5, dov, a.nout, k, m, a.ld_d);
+        const float xh = (gelu_f(u[(long long)k * a.ld + m]) - mu) * rs;
+        const float dxh = dhv * gam[k];
+        s1 += dxh;
+        s2 += dxh * xh;
+    }
+    __shared__ float red[2][4][64];
+    red[0][w][lane] = s1;
+    red[1][w][lane] = s2;
+    __syncthreads();
+    if (w == 0) {
+        const float S1 = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
+        const float S2 = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+        at(a.c1, slot, y)[m] = S1 / (float)a.H;
+        at(a.c2, slot, y)[m] = S2 / (float)a.H;
+    }
+}
+
+// One wave per feature k: du'[k][m] for every column m, plus the parameter
+// gradients that are sums over the batch (only columns m < Mg contribute):
+//   bias  db[k] = sum du ;  LN: dgamma[k] = sum dh*xhat, dbeta[k] = sum dh ;
+//   head: dW5[k][j] = sum x_head[k][m] dout[j][m].
+template <bool HEAD, bool LN>
+__global__ __launch_bounds__(256) void bwd_cols_kernel(const BwdArgs a) {
+    const int nkb = a.H / 4;
+    const int kb = blockIdx.x % nkb, yz = blockIdx.x / nkb;
+    const int y = yz % a.ny, z = yz / a.ny;
+    const int slot = a.slots[z];
+    const int lane = threadIdx.x & 63;
+    const int k = kb * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const float* __restrict__ u = at(a.u, slot, y);
+    const float* __restrict__ dh = HEAD ? nullptr : at(a.dh, slot, y);
+    const float* __restrict__ W5 = HEAD ? at(a.W5, slot, y) : nullptr;
+    const float* __restrict__ dout = HEAD ? at(a.dout, slot, y) : nullptr;
+    const float* __restrict__ xhd = HEAD ? at(a.x_head, slot, y) : nullptr;
+    const float* __restrict__ mu = LN ? at(a.mu, slot, y) : nullptr;
+    const float* __restrict__ rs = LN ? at(a.rstd, slot, y) : nullptr;
+    const float* __restrict__ c1 = LN ? at(a.c1, slot, y) : nullptr;
+    const float* __restrict__ c2 = LN ? at(a.c2, slot, y) : nullptr;
+    const float gam = LN ? at(a.gamma, slot, y)[k] : 1.f;
+    float* __restrict__ du = at(a.du, slot, y);
+    float sb = 0.f, sg = 0.f, sbeta = 0.f;
+    float sw[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sw[j] = 0.f;
+    for (int m = lane; m < a.M; m += 64) {
+        float dov[8];
+        if constexpr (HEAD) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dov[j] = (j < a.nout) ? dout[(long long)j * a.ld_o + m] : 0.f;
+        }
+        const float dhv = load_dh<HEAD>(dh, W5, dov, a.nout, k, m, a.ld_d);
+        const float uv = u[(long long)k * a.ld + m];
+        float dg;
+        if constexpr (LN) {
+            const float xh = (gelu_f(uv) - mu[m]) * rs[m];
+            dg = rs[m] * (dhv * gam - c1[m] - xh * c2[m]);
+            if (m < a.Mg) {
+                sg += dhv * xh;
+                sbeta += dhv;
+            }
+        } else {
+            dg = dhv;
+        }
+        const float duv = dg * gelu_grad_f(uv);
+        du[(long long)k * a.ld_d + m] = duv;
+        if (m < a.Mg) {
+            sb += duv;
+            if constexpr (HEAD) {
+                const float xv = xhd[(long long)k * a.ld + m];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) sw[j] += xv * dov[j];
+            }
+        }
+    }
+    sb = wave_sum(sb);
+    if constexpr (LN) {
+        sg = wave_sum(sg);
+        sbeta = wave_sum(sbeta);
+    }
+    if constexpr (HEAD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sw[j] = wave_sum(sw[j]);
+    }
+    if (lane == 0) {
+        at(a.g_b, slot, y)[k] = sb;
+        if constexpr (LN) {
+            at(a.g_gamma, slot, y)[k] = sg;
+            at(a.g_beta, slot, y)[k] = sbeta;
+        }
+        if constexpr (HEAD) {
+            float* gw = at(a.g_W5, slot, y) + (long long)k * a.nout;
+            for (int j = 0; j < a.nout; ++j) gw[j] = sw[j];
+        }
+    }
+}
+
+void launch_bwd_rowstats(bool head, const BwdArgs& a, hipStream_t s) {
+    const dim3 grid((a.M / 64) * a.ny * a.nz), blk(256);
+    if (head) hipLaunchKernelGGL(bwd_rowstats_kernel<true>, grid, blk, 0, s, a);
+    else hipLaunchKernelGGL(bwd_rowstats_kernel<false>, grid, blk, 0, s, a);
+}
+
+void launch_bwd_cols(bool head, bool ln, const BwdArgs& a, hipStream_t s) {
+    const dim3 grid((a.H / 4) * a.ny * a.nz), blk(256);
+    if (head && ln) hipLaunchKernelGGL((bwd_cols_kernel<true, true>), grid, blk, 0, s, a);
+    else if (head) hipLaunchKernelGGL((bwd_cols_kernel<true, false>), grid, blk, 0, s, a);
+    else if (ln) hipLaunchKernelGGL((bwd_cols_kernel<false, true>), grid, blk, 0, s, a);
+    else hipLaunchKernelGGL((bwd_cols_kernel<false, false>), grid, blk, 0, s, a);
+}
+
+// dq/da for the actor's Q term: the critic's first-layer input gradient,
+// restricted to the action rows and summed over the ensemble.
+__global__ __launch_bounds__(256) void input_grad_kernel(const InGradArgs a) {
+    const int ncb = a.M / 64;
+    const int cb = blockIdx.x % ncb, z = blockIdx.x / ncb;
+    const int slot = a.slots[z];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m = cb * 64 + lane;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    const int nq = a.H / 4, n0 = w * nq;
+    for (int e = 0; e < a.E; ++e) {
+        const float* __restrict__ W0 = at(a.W0, slot, e);
+        const float* __restrict__ du = at(a.du0, slot, e);
+        for (int n = n0; n < n0 + nq; ++n) {
+            const float dv = du[(long long)n * a.ld + a.off + m];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < a.A) acc[j] += W0[(long long)(a.D + j) * a.H + n] * dv;
+        }
+    }
+    __shared__ float red[4][8][64];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[w][j][lane] = acc[j];
+    __syncthreads();
+    if (w == 0) {
+        float* da = at(a.da, slot);
+        for (int j = 0; j < a.A; ++j)
+            da[(long long)j * a.M + m] = (red[0][j][lane] + red[1][j][lane]) + (red[2][j][lane] + red[3][j][lane]);
+    }
+}
+
+void launch_input_grad(const InGradArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(input_grad_kernel, dim3((a.M / 64) * a.nz), dim3(256), 0, s, a);
+}
+
+// =============================================================== RNG =======
+// Philox4x32-10 (Salmon et al. 2011), counter = (row, step, salt, word).
+DEV void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+DEV float u01_open_closed(uint32_t x) { return ((x >> 8) + 1u) * (1.0f / 16777216.0f); }  // (0,1]
+DEV float u01(uint32_t x) { return (x >> 8) * (1.0f / 16777216.0f); }                    // [0,1)
+
+// Normals n[0..cnt) for (row, step, salt), words 1.. of the Philox stream.
+DEV void philox_normals(float* n, int cnt, uint64_t seed, uint32_t row, uint32_t step, uint32_t salt) {
+    for (int i = 0; i < cnt; i += 2) {
+        uint32_t c[4] = {row, step, salt, 1u + (uint32_t)(i >> 1)};
+        philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        const float r = sqrtf(-2.0f * logf(u01_open_closed(c[0])));
+        float sv, cv;
+        sincosf(6.283185307179586f * u01(c[1]), &sv, &cv);
+        n[i] = r * cv;
+        if (i + 1 < cnt) n[i + 1] = r * sv;
+    }
+}
+
+// ============================================================ sampling =====
+// Minibatch draw (uniform with replacement, [EXT] Dataset.sample) + noise
+// draws + assembly of every network's first-layer input (feature-major
+// concatenation = stacking row blocks).  Injected mode reads batch/noise from
+// a packed staging buffer instead (parity tests).
+__global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
+    const int nbb = (a.B + 255) / 256;
+    const int bb = blockIdx.x % nbb, z = blockIdx.x / nbb;
+    const int slot = a.slots[z];
+    const int b = bb * 256 + threadIdx.x;
+    if (b >= a.B) return;
+    const int B = a.B, D = a.D, A = a.A;
+    float zn[8], x0[8], zd[8], zm[8], act[8];
+    float t, rew, mask;
+    const float *obs, *nobs;
+    if (a.inj_batch) {
+        const long long bs = (long long)B * (2 * D + A + 2), ns = (long long)B * (4 * A + 1);
+        const float* pb = a.inj_batch + z * bs;
+        const float* pn = a.inj_noise + z * ns;
+        obs = pb + (long long)b * D;
+        const float* pa = pb + (long long)B * D;
+        rew = pb[(long long)B * (D + A) + b];
+        mask = pb[(long long)B * (D + A + 1) + b];
+        nobs = pb + (long long)B * (D + A + 2) + (long long)b * D;
+        for (int j = 0; j < A; ++j) {
+            act[j] = pa[b * A + j];
+            zn[j] = pn[b * A + j];
+            x0[j] = pn[(long long)B * A + b * A + j];
+            zd[j] = pn[(long long)B * (2 * A + 1) + b * A + j];
+            zm[j] = pn[(long long)B * (3 * A + 1) + b * A + j];
+        }
+        t = pn[(long long)B * 2 * A + b];
+    } else {
+        const uint64_t seed = a.seeds[slot];
+        const uint32_t step = (uint32_t)a.count[slot];
+        uint32_t c[4] = {(uint32_t)b, step, a.stream_salt, 0u};
+        philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        const long long idx = (long long)(((unsigned long long)c[0] * (unsigned long long)a.n_rows) >> 32);
+        t = u01(c[1]);
+        float nrm[32];
+        philox_normals(nrm, 4 * A, seed, (uint32_t)b, step, a.stream_salt);
+        for (int j = 0; j < A; ++j) {
+            zn[j] = nrm[j];
+            x0[j] = nrm[A + j];
+            zd[j] = nrm[2 * A + j];
+            zm[j] = nrm[3 * A + j];
+            act[j] = a.act[idx * A + j];
+        }
+        obs = a.obs + idx * D;
+        nobs = a.nobs + idx * D;
+        rew = a.rew[idx];
+        mask = a.mask[idx];
+    }
+    float* os = at(a.os_in, slot);
+    float* bc = at(a.bc_in, slot);
+    float* cr = at(a.cr_in, slot);
+    float* tg = at(a.tg_in, slot);
+    float* eu = at(a.eu_in, slot);
+    const long long B2 = 2 * (long long)B, B3 = 3 * (long long)B;
+    for (int k = 0; k < D; ++k) {
+        const float o = obs[k], n = nobs[k];
+        os[k * B3 + b] = n;
+        os[k * B3 + B + b] = o;
+        os[k * B3 + 2 * B + b] = o;
+        bc[k * B2 + b] = o;
+        bc[k * B2 + B + b] = o;
+        cr[k * B2 + b] = o;
+        cr[k * B2 + B + b] = o;
+        tg[(long long)k * B + b] = n;
+        eu[(long long)k * B + b] = o;
+    }
+    float* at_ = at(a.act_t, slot);
+    float* x0_ = at(a.x0_t, slot);
+    for (int j = 0; j < A; ++j) {
+        const long long r = D + j;
+        os[r * B3 + b] = zn[j];
+        os[r * B3 + B + b] = zd[j];
+        os[r * B3 + 2 * B + b] = zm[j];
+        bc[r * B2 + b] = (1.0f - t) * x0[j] + t * act[j];
+        bc[r * B2 + B + b] = zd[j];
+        cr[r * B2 + b] = act[j];
+        at_[(long long)j * B + b] = act[j];
+        x0_[(long long)j * B + b] = x0[j];
+    }
+    bc[(long long)(D + A) * B2 + b] = t;
+    bc[(long long)(D + A) * B2 + B + b] = 0.0f;
+    at(a.rew_t, slot)[b] = rew;
+    at(a.mask_t, slot)[b] = mask;
+}
+
+void launch_sample(const SampleArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(sample_kernel, dim3(((a.B + 255) / 256) * a.nz), dim3(256), 0, s, a);
+}
+
+// =============================================================== losses ====
+// [EXT] critic_loss: y = r + gamma*mask*agg_k Qt_k(s',a'); L = mean (Q-y)^2
+// over [E,B]; also the Q-term of actor_loss (q = mean_k Q_k(s, clip(a_pi))),
+// its gradient seeds, and the mse metric.  One block per member.
+__global__ __launch_bounds__(256) void loss_critic_kernel(const LossArgs a) {
+    const int z = blockIdx.x, slot = a.slots[z];
+    const int B = a.B, E = a.E, A = a.A;
+    __shared__ float red[4];
+    const float* q = at(a.q, slot);      // [E][2B] (ens stride = q.sy)
+    const float* qt = at(a.qt, slot);    // [E][B]
+    const float* rw = at(a.rew, slot);
+    const float* mk = at(a.mask, slot);
+    float* dq = at(a.dq, slot);
+    const float invEB = 1.0f / (float)(E * B);
+    float sq = 0.f, qs = 0.f, qmx = -INFINITY, qmn = INFINITY, qpi_s = 0.f, qpi_abs = 0.f;
+    float sdq[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int b = threadIdx.x; b < B; b += 256) {
+        float agg = a.q_min ? INFINITY : 0.f;
+        for (int e = 0; e < E; ++e) {
+            const float v = qt[e * a.qt.sy + b];
+            agg = a.q_min ? fminf(agg, v) : agg + v;
+        }
+        if (!a.q_min) agg /= (float)E;
+        const float y = rw[b] + a.discount * mk[b] * agg;
+        float qp = 0.f;
+        for (int e = 0; e < E; ++e) {
+            const float qv = q[e * a.q.sy + b];
+            const float d = qv - y;
+            sq += d * d;
+            qs += qv;
+            qmx = fmaxf(qmx, qv);
+            qmn = fminf(qmn, qv);
+            const float g = 2.0f * d * invEB;
+            dq[e * a.dq.sy + b] = g;
+            if (e < 4) sdq[e] += g;
+            qp += q[e * a.q.sy + B + b];
+        }
+        qp /= (float)E;
+        qpi_s += qp;
+        qpi_abs += fabsf(qp);
+    }
+    // mse metric of sample_actions(s) against the dataset actions
+    const float* am = at(a.amet, slot);
+    const float* ac = at(a.act, slot);
+    float smse = 0.f;
+    for (int i = threadIdx.x; i < A * B; i += 256) {
+        const float d = am[i] - ac[i];
+        smse += d * d;
+    }
+    sq = block_sum(sq, red);
+    qs = block_sum(qs, red);
+    qmx = block_max(qmx, red);
+    qmn = block_min(qmn, red);
+    qpi_s = block_sum(qpi_s, red);
+    qpi_abs = block_sum(qpi_abs, red);
+    smse = block_sum(smse, red);
+    for (int e = 0; e < E && e < 4; ++e) {
+        const float s = block_sum(sdq[e], red);
+        if (threadIdx.x == 0) at(a.g_cb4, slot, e)[0] = s;
+    }
+    const float qmean_pi = qpi_s / (float)B;
+    const float lam = a.normq ? 1.0f / (qpi_abs / (float)B) : 1.0f;
+    const float gpi = -lam * invEB;
+    for (int b = threadIdx.x; b < B; b += 256)
+        for (int e = 0; e < E; ++e) dq[e * a.dq.sy + B + b] = gpi;
+    if (threadIdx.x == 0) {
+        float* info = at(a.info, slot);
+        info[0] = sq * invEB;
+        info[1] = qs * invEB;
+        info[2] = qmx;
+        info[3] = qmn;
+        info[7] = -lam * qmean_pi;
+        info[8] = qmean_pi;
+        info[9] = smse / (float)(A * B);
+    }
+}
+
+// [EXT] BC flow-matching loss: mean over [B,A] of (v_theta(s,x_t,t) - (a - x0))^2.
+__global__ __launch_bounds__(256) void loss_bc_kernel(const LossArgs a) {
+    const int z = blockIdx.x, slot = a.slots[z];
+    const int B = a.B, A = a.A;
+    __shared__ float red[4];
+    const float* vp = at(a.vpred, slot);
+    const float* ac = at(a.act, slot);
+    const float* x0 = at(a.x0, slot);
+    float* dv = at(a.dv, slot);
+    const float sc = 2.0f / (float)(A * B);
+    float s = 0.f;
+    float sdb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sdb[j] = 0.f;
+    for (int b = threadIdx.x; b < B; b += 256) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j < A) {
+                const long long o = (long long)j * B + b;
+                const float d = vp[o] - (ac[o] - x0[o]);
+                s += d * d;
+                const float g = sc * d;
+                dv[o] = g;
+                sdb[j] += g;
+            }
+        }
+    }
+    s = block_sum(s, red);
+    for (int j = 0; j < A; ++j) {
+        const float t = block_sum(sdb[j], red);
+        if (threadIdx.x == 0) at(a.g_bcb4, slot)[j] = t;
+    }
+    if (threadIdx.x == 0) at(a.info, slot)[5] = s / (float)(A * B);
+}
+
+// [EXT] actor_loss remainder: distill = mean (a_pi - a_flow)^2; the onestep
+// output gradient alpha*d(distill) + 1{-1<a_pi<1} * dq/da (clip passes no
+// gradient outside); actor_loss = bc + alpha*distill + q_loss.
+__global__ __launch_bounds__(256) void loss_actor_kernel(const LossArgs a) {
+    const int z = blockIdx.x, slot = a.slots[z];
+    const int B = a.B, A = a.A;
+    __shared__ float red[4];
+    const float alpha = a.alpha[slot];
+    const float* ap = at(a.apiraw, slot);
+    const float* af = at(a.aflow, slot);
+    const float* da = at(a.da, slot);
+    float* dout = at(a.dout_os, slot);
+    const float sc = 2.0f / (float)(A * B);
+    float s = 0.f;
+    float sdb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sdb[j] = 0.f;
+    for (int b = threadIdx.x; b < B; b += 256) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j < A) {
+                const long long o = (long long)j * B + b;
+                const float x = ap[o];
+                const float d = x - af[o];
+                s += d * d;
+                const float g = alpha * (sc * d) + ((x > -1.0f && x < 1.0f) ? da[o] : 0.0f);
+                dout[o] = g;
+                sdb[j] += g;
+            }
+        }
+    }
+    s = block_sum(s, red);
+    for (int j = 0; j < A; ++j) {
+        const float t = block_sum(sdb[j], red);
+        if (threadIdx.x == 0) at(a.g_osb4, slot)[j] = t;
+    }
+    if (threadIdx.x == 0) {
+        float* info = at(a.info, slot);
+        const float distill = s / (float)(A * B);
+        info[6] = distill;
+        info[4] = info[5] + alpha * distill + info[7];
+    }
+}
+
+void launch_loss_critic(const LossArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(loss_critic_kernel, dim3(a.nz), dim3(256), 0, s, a);
+}
+void launch_loss_bc(const LossArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(loss_bc_kernel, dim3(a.nz), dim3(256), 0, s, a);
+}
+void launch_loss_actor(const LossArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(loss_actor_kernel, dim3(a.nz), dim3(256), 0, s, a);
+}
+
+// ============================================================ optimiser ====
+// optax.adam(lr) (b1 .9, b2 .999, eps 1e-8 outside the sqrt, bias correction
+// with count+1) fused with the target-critic EMA (from the PRE-update critic)
+// and the per-chunk grad statistics of apply_loss_fn (max, min, sum g^2).
+__global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
+    const int ci = blockIdx.x, z = blockIdx.y;
+    const int slot = a.slots[z];
+    const Chunk ck = a.chunks[ci];
+    const long long base = (long long)slot * a.P + a.net_off + ck.off;
+    float* __restrict__ P = a.p + base;
+    const float* __restrict__ G = a.g + base;
+    float* __restrict__ Mm = a.m + base;
+    float* __restrict__ V = a.v + base;
+    float* __restrict__ T = a.target ? a.target + (long long)slot * a.PT + ck.off : nullptr;
+    const float t = (float)(a.count[slot] + 1);
+    const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
+    float mx = -INFINITY, mn = INFINITY, ss = 0.f;
+    const float lr = a.lr, tau = a.tau;
+    // one Adam element (+ EMA of the target from the pre-update value)
+#define FQ_ADAM1(g, p, m, v, hasT, tp)                              \
+    do {                                                            \
+        m = 0.1f * (g) + 0.9f * m;                                  \
+        v = 0.001f * ((g) * (g)) + 0.999f * v;                      \
+        const float mh_ = m / bc1, vh_ = v / bc2;                   \
+        if (hasT) tp = tau * p + (1.0f - tau) * tp;                 \
+        p = p + (-lr) * (mh_ / (sqrtf(vh_) + 1e-8f));               \
+        mx = fmaxf(mx, (g));                                        \
+        mn = fminf(mn, (g));                                        \
+        ss += (g) * (g);                                            \
+    } while (0)
+    const bool hasT = T != nullptr;
+    if ((ck.len & 3) == 0) {
+        for (int i = threadIdx.x * 4; i < ck.len; i += 1024) {
+            const float4 g4 = *reinterpret_cast<const float4*>(G + i);
+            float4 p4 = *reinterpret_cast<float4*>(P + i);
+            float4 m4 = *reinterpret_cast<float4*>(Mm + i);
+            float4 v4 = *reinterpret_cast<float4*>(V + i);
+            float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (hasT) t4 = *reinterpret_cast<float4*>(T + i);
+            FQ_ADAM1(g4.x, p4.x, m4.x, v4.x, hasT, t4.x);
+            FQ_ADAM1(g4.y, p4.y, m4.y, v4.y, hasT, t4.y);
+            FQ_ADAM1(g4.z, p4.z, m4.z, v4.z, hasT, t4.z);
+            FQ_ADAM1(g4.w, p4.w, m4.w, v4.w, hasT, t4.w);
+            *reinterpret_cast<float4*>(P + i) = p4;
+            *reinterpret_cast<float4*>(Mm + i) = m4;
+            *reinterpret_cast<float4*>(V + i) = v4;
+            if (hasT) *reinterpret_cast<float4*>(T + i) = t4;
+        }
+    } else {
+        for (int i = threadIdx.x; i < ck.len; i += 256) {
+            const float gv = G[i];
+            float p = P[i], m = Mm[i], v = V[i], tv = hasT ? T[i] : 0.f;
+            FQ_ADAM1(gv, p, m, v, hasT, tv);
+            P[i] = p;
+            Mm[i] = m;
+            V[i] = v;
+            if (hasT) T[i] = tv;
+        }
+    }
+#undef FQ_ADAM1
+    __shared__ float red[4];
+    mx = block_max(mx, red);
+    mn = block_min(mn, red);
+    ss = block_sum(ss, red);
+    if (threadIdx.x == 0) {
+        float* st = a.stats + ((long long)slot * a.n_total_chunks + a.chunk_base + ci) * 3;
+        st[0] = mx;
+        st[1] = mn;
+        st[2] = ss;
+    }
+}
+
+void launch_adam(const AdamArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(adam_kernel, dim3(a.n_chunks, a.nz), dim3(256), 0, s, a);
+}
+
+// grad/max, grad/min over every leaf (target-critic leaves contribute zeros),
+// grad/norm = sum over leaves of the leaf L2 norm; count += 1.
+__global__ __launch_bounds__(64) void finalize_kernel(const FinalArgs a) {
+    const int z = blockIdx.x, slot = a.slots[z];
+    __shared__ float leaf_ss[128];
+    for (int i = threadIdx.x; i < 128; i += 64) leaf_ss[i] = 0.f;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float* st = a.stats + (long long)slot * a.n_total_chunks * 3;
+        float mx = 0.f, mn = 0.f;  // zero target-critic leaves are part of the tree
+        for (int c = 0; c < a.n_total_chunks; ++c) {
+            mx = fmaxf(mx, st[c * 3 + 0]);
+            mn = fminf(mn, st[c * 3 + 1]);
+            leaf_ss[a.chunk_leaf[c]] += st[c * 3 + 2];
+        }
+        float nrm = 0.f;
+        for (int l = 0; l < a.n_leaves; ++l) nrm += sqrtf(leaf_ss[l]);
+        float* info = at(a.info, slot);
+        info[10] = mx;
+        info[11] = mn;
+        info[12] = nrm;
+        a.count[slot] += 1;
+    }
+}
+
+void launch_finalize(const FinalArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(a.nz), dim3(64), 0, s, a);
+}
+
+// ================================================================= init ====
+__global__ __launch_bounds__(256) void init_kernel(const InitArgs a) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    if (a.lim == 0.f) {
+        a.p[i] = a.value;
+        return;
+    }
+    uint32_t c[4] = {(uint32_t)i, (uint32_t)(i >> 32), a.salt, 0xF1A5u};
+    philox4x32_10(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+    a.p[i] = (2.0f * u01(c[0]) - 1.0f) * a.lim;
+}
+
+void launch_init(const InitArgs& a, hipStream_t s) {
+    if (a.n <= 0) return;
+    hipLaunchKernelGGL(init_kernel, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+}
+
+}  // namespace fq

@@ -1,0 +1,1161 @@
+// Host runtime of libfqlpop.so: the C ABI of include/fqlpop.h.
+//
+// One handle = one population on one GPU.  The handle owns every device
+// buffer (params / grads / Adam moments / target critic arenas, activations,
+// datasets) and three HIP streams that carry the update DAG of one population
+// step:
+//   sF  flow chain : BC-flow forward fused with Euler step 0, Euler steps 1..S-1
+//   sB  BC branch  : BC loss, BC backward, BC Adam (after the flow chain)
+//   sM  main chain : sampling, one-step actor forward, critic/target forward,
+//                    critic loss + backward + Adam/EMA, actor loss (joins sF),
+//                    one-step backward + Adam, grad stats (joins sB)
+// The whole DAG is captured once into a hipGraph and replayed per step.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/fqlpop.h"
+#include "kernels.h"
+
+using namespace fq;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct FqErr {
+    int code;
+    std::string msg;
+};
+
+#define HIPCHK(x)                                                                                 \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess)                                                                     \
+            throw FqErr{FQLPOP_E_HIP, std::string(#x) + " failed: " + hipGetErrorString(e_)};     \
+    } while (0)
+
+#define ARGCHK(c, m)                                         \
+    do {                                                     \
+        if (!(c)) throw FqErr{FQLPOP_E_ARG, std::string(m)}; \
+    } while (0)
+
+constexpr long long kAlign = 64;  // floats (256 B)
+long long align_up(long long x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+// ---------------------------------------------------------------- host Philox
+void philox_host(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+// ---------------------------------------------------------------- layout
+// Parameter block of one network, flax MLP naming: Dense_l (kernel [in][out],
+// bias [out]) and LayerNorm_l (scale, bias) after every hidden Dense.
+struct NetLayout {
+    std::string name;
+    int in_dim = 0, out_dim = 0, L = 0, H = 0, E = 1;
+    bool ln = false;
+    long long off = 0;        // offset of the net inside its arena
+    long long ens_size = 0;   // floats of one ensemble member (aligned)
+    std::vector<long long> W, b, gam, bet;  // offsets inside one ensemble member
+    int kdim(int l) const { return l == 0 ? in_dim : H; }
+    int ndim(int l) const { return l == L ? out_dim : H; }
+
+    void build(const std::string& nm, int in, int out, int nh, int h, int e, bool use_ln) {
+        name = nm; in_dim = in; out_dim = out; L = nh; H = h; E = e; ln = use_ln;
+        long long o = 0;
+        for (int l = 0; l <= L; ++l) {
+            W.push_back(o); o = align_up(o + (long long)kdim(l) * ndim(l));
+            b.push_back(o); o = align_up(o + ndim(l));
+            if (l < L && ln) {
+                gam.push_back(o); o = align_up(o + H);
+                bet.push_back(o); o = align_up(o + H);
+            }
+        }
+        ens_size = o;
+    }
+    long long size() const { return ens_size * E; }
+};
+
+// Leaf of the flax-ordered flat state.
+struct Leaf {
+    std::string name;
+    int net;          // 0 critic, 1 target, 2 bc, 3 os  (internal ids)
+    int kind;         // 0 kernel, 1 bias, 2 LN scale, 3 LN bias
+    int layer;
+    int ndim;
+    long long shape[3];
+    long long flat_off;
+    long long size;
+};
+
+struct Graphs {
+    hipGraphExec_t exec = nullptr;
+    int nz = -1;
+};
+
+}  // namespace
+
+struct fqlpop {
+    fqlpop_config cfg{};
+    int n = 0;          // slots
+    int device = 0;
+    int D = 0, A = 0, H = 0, L = 0, B = 0, E = 0, S = 0;
+    NetLayout critic, bc, os;   // critic at arena offset 0 (target arena mirrors it)
+    long long P = 0, PT = 0;    // per-slot arena sizes
+    std::vector<Leaf> leaves;
+    long long state_size = 0;
+
+    // device state
+    float *params = nullptr, *grads = nullptr, *adam_m = nullptr, *adam_v = nullptr, *target = nullptr;
+    int* count = nullptr;
+    uint64_t* seeds = nullptr;
+    float* alpha = nullptr;
+    int* slots = nullptr;
+    float* stats = nullptr;
+    Chunk* chunks = nullptr;
+    int* chunk_leaf = nullptr;
+    int n_chunks_net[3] = {0, 0, 0}, chunk_base_net[3] = {0, 0, 0}, n_chunks_total = 0;
+    int n_train_leaves = 0;
+
+    // host mirror
+    std::vector<float> h_alpha;
+    std::vector<uint64_t> h_seeds;
+    std::vector<uint8_t> active;
+    std::vector<int> h_slots;
+    int nz = 0;
+
+    // datasets
+    struct Dataset {
+        float *obs = nullptr, *act = nullptr, *rew = nullptr, *mask = nullptr, *nobs = nullptr;
+        long long rows = 0;
+    } ds[2];
+
+    // activations (slot-strided)
+    std::vector<float*> allocs;
+    float *os_in, *bc_in, *eu_in, *cr_in, *tg_in;
+    std::vector<float*> os_u, os_g, bc_u, bc_g, eu_g, cr_u, cr_h, cr_mu, cr_rs, tg_u, tg_h, tg_mu, tg_rs;
+    std::vector<float*> cr_du, bc_du, os_du;
+    float *cr_dh, *bc_dh, *os_dh, *cr_c1, *cr_c2;
+    float *q, *qt, *dq, *vpred, *dv, *act_t, *x0_t, *rew_t, *mask_t, *apiraw, *aflow, *amet, *da, *dout_os;
+    float *info, *vinfo;
+    float *inj_batch = nullptr, *inj_noise = nullptr;
+    long long inj_bs = 0, inj_ns = 0;
+
+    hipStream_t sM = nullptr, sF = nullptr, sB = nullptr;
+    hipEvent_t ev_sample, ev_bcfwd, ev_bcloss, ev_flow, ev_bdone, ev_t0, ev_t1;
+    std::map<int, Graphs> graphs;  // key: train*2 + injected
+
+    float* alloc(long long per_slot) {
+        float* p = nullptr;
+        HIPCHK(hipMalloc(&p, sizeof(float) * std::max<long long>(1, per_slot * n)));
+        HIPCHK(hipMemset(p, 0, sizeof(float) * std::max<long long>(1, per_slot * n)));
+        allocs.push_back(p);
+        return p;
+    }
+};
+
+namespace {
+
+// ------------------------------------------------------------- leaves/chunks
+void build_leaves(fqlpop* h) {
+    // flax ModuleDict order: modules_actor_bc_flow, modules_actor_onestep_flow,
+    // modules_critic, modules_target_critic; leaves sorted by path.
+    struct NetRef { const char* name; int id; const NetLayout* lay; };
+    const NetRef order[4] = {{"actor_bc_flow", 2, &h->bc}, {"actor_onestep_flow", 3, &h->os},
+                             {"critic", 0, &h->critic}, {"target_critic", 1, &h->critic}};
+    long long off = 0;
+    for (const auto& nr : order) {
+        const NetLayout& N = *nr.lay;
+        std::vector<Leaf> ls;
+        for (int l = 0; l <= N.L; ++l) {
+            for (int kind = 0; kind < 2; ++kind) {
+                Leaf lf{};
+                lf.net = nr.id; lf.kind = kind; lf.layer = l;
+                lf.name = std::string(nr.name) + "/Dense_" + std::to_string(l) + (kind == 0 ? "/kernel" : "/bias");
+                std::vector<long long> shp;
+                if (N.E > 1) shp.push_back(N.E);
+                if (kind == 0) shp.push_back(N.kdim(l));
+                shp.push_back(N.ndim(l));
+                lf.ndim = (int)shp.size();
+                lf.size = 1;
+                for (int i = 0; i < lf.ndim; ++i) { lf.shape[i] = shp[i]; lf.size *= shp[i]; }
+                ls.push_back(lf);
+            }
+            if (l < N.L && N.ln) {
+                for (int kind = 2; kind < 4; ++kind) {
+                    Leaf lf{};
+                    lf.net = nr.id; lf.kind = kind; lf.layer = l;
+                    lf.name = std::string(nr.name) + "/LayerNorm_" + std::to_string(l) + (kind == 2 ? "/scale" : "/bias");
+                    lf.ndim = N.E > 1 ? 2 : 1;
+                    lf.shape[0] = N.E > 1 ? N.E : N.H;
+                    if (N.E > 1) lf.shape[1] = N.H;
+                    lf.size = (long long)N.E * N.H;
+                    ls.push_back(lf);
+                }
+            }
+        }
+        std::sort(ls.begin(), ls.end(), [](const Leaf& a, const Leaf& b) { return a.name < b.name; });
+        for (auto& lf : ls) { lf.flat_off = off; off += lf.size; h->leaves.push_back(lf); }
+    }
+    h->state_size = off;
+}
+
+long long leaf_internal_off(const NetLayout& N, int kind, int layer) {
+    switch (kind) {
+        case 0: return N.W[layer];
+        case 1: return N.b[layer];
+        case 2: return N.gam[layer];
+        default: return N.bet[layer];
+    }
+}
+
+// per-ensemble-member element count of a leaf
+long long leaf_member_size(const NetLayout& N, int kind, int layer) {
+    if (kind == 0) return (long long)N.kdim(layer) * N.ndim(layer);
+    if (kind == 1) return N.ndim(layer);
+    return N.H;
+}
+
+void build_chunks(fqlpop* h) {
+    constexpr int CH = 16384;
+    std::vector<Chunk> all;
+    std::vector<int> all_leaf;
+    const NetLayout* nets[3] = {&h->critic, &h->bc, &h->os};
+    int leaf_id = 0;
+    for (int ni = 0; ni < 3; ++ni) {
+        const NetLayout& N = *nets[ni];
+        h->chunk_base_net[ni] = (int)all.size();
+        for (int l = 0; l <= N.L; ++l) {
+            for (int kind = 0; kind < 4; ++kind) {
+                if (kind >= 2 && (l == N.L || !N.ln)) continue;
+                const long long len = leaf_member_size(N, kind, l);
+                for (int e = 0; e < N.E; ++e) {
+                    const long long base = e * N.ens_size + leaf_internal_off(N, kind, l);
+                    for (long long s = 0; s < len; s += CH) {
+                        Chunk c;
+                        c.off = base + s;
+                        c.len = (int)std::min<long long>(CH, len - s);
+                        c.leaf = leaf_id;
+                        all.push_back(c);
+                        all_leaf.push_back(leaf_id);
+                    }
+                }
+                ++leaf_id;
+            }
+        }
+        h->n_chunks_net[ni] = (int)all.size() - h->chunk_base_net[ni];
+    }
+    h->n_chunks_total = (int)all.size();
+    h->n_train_leaves = leaf_id;
+    ARGCHK(leaf_id <= 128, "too many leaves");
+    HIPCHK(hipMalloc(&h->chunks, sizeof(Chunk) * all.size()));
+    HIPCHK(hipMemcpy(h->chunks, all.data(), sizeof(Chunk) * all.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&h->chunk_leaf, sizeof(int) * all_leaf.size()));
+    HIPCHK(hipMemcpy(h->chunk_leaf, all_leaf.data(), sizeof(int) * all_leaf.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&h->stats, sizeof(float) * 3 * all.size() * h->n));
+    HIPCHK(hipMemset(h->stats, 0, sizeof(float) * 3 * all.size() * h->n));
+}
+
+// ------------------------------------------------------------- params init
+void init_member(fqlpop* h, int slot, uint64_t seed) {
+    unsigned salt = 1;
+    auto init_net = [&](const NetLayout& N) {
+        for (int e = 0; e < N.E; ++e) {
+            float* base = h->params + (long long)slot * h->P + N.off + e * N.ens_size;
+            for (int l = 0; l <= N.L; ++l) {
+                const int fi = N.kdim(l), fo = N.ndim(l);
+                InitArgs a{base + N.W[l], (long long)fi * fo, std::sqrt(6.0f / (float)(fi + fo)), 0.f, seed, salt++};
+                launch_init(a, h->sM);
+                InitArgs ab{base + N.b[l], fo, 0.f, 0.f, seed, salt++};
+                launch_init(ab, h->sM);
+                if (l < N.L && N.ln) {
+                    InitArgs ag{base + N.gam[l], N.H, 0.f, 1.f, seed, salt++};
+                    launch_init(ag, h->sM);
+                    InitArgs abt{base + N.bet[l], N.H, 0.f, 0.f, seed, salt++};
+                    launch_init(abt, h->sM);
+                }
+            }
+        }
+    };
+    init_net(h->critic);
+    init_net(h->bc);
+    init_net(h->os);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemsetAsync(h->adam_m + (long long)slot * h->P, 0, sizeof(float) * h->P, h->sM));
+    HIPCHK(hipMemsetAsync(h->adam_v + (long long)slot * h->P, 0, sizeof(float) * h->P, h->sM));
+    HIPCHK(hipMemcpyAsync(h->target + (long long)slot * h->PT, h->params + (long long)slot * h->P,
+                          sizeof(float) * h->PT, hipMemcpyDeviceToDevice, h->sM));
+    HIPCHK(hipMemsetAsync(h->count + slot, 0, sizeof(int), h->sM));
+    HIPCHK(hipStreamSynchronize(h->sM));
+}
+
+// ------------------------------------------------------------- DAG helpers
+struct Ctx {
+    fqlpop* h;
+    int nz;
+};
+
+TRef pref(fqlpop* h, float* arena, const NetLayout& N, long long off) {
+    return tref(arena + N.off + off, h->P, N.ens_size);
+}
+
+int pick_tile(int M, int N, int nyz) {
+    // 64x64 gives the most workgroups; use bigger tiles only when the launch
+    // alone has several waves of workgroups for 256 CUs.
+    const long long t64 = (long long)((M + 63) / 64) * ((N + 63) / 64) * nyz;
+    if (t64 >= 2048) return 3;
+    if (t64 >= 1024) return 1;
+    return 0;
+}
+
+// Forward of the hidden stack of `N` over `M` columns of input X (ld = ldx).
+// U[l]/G[l]: pre-activation and layer output buffers (ld = ldx).  store_u:
+// keep u (needed by backward / LN); otherwise G[l] = gelu(u) directly.
+void fwd_hidden(const Ctx& c, hipStream_t s, const NetLayout& N, TRef X, int ldx, int M,
+                const std::vector<float*>& U, const std::vector<float*>& G, long long act_sy,
+                const std::vector<float*>* MU, const std::vector<float*>* RS, long long st_sy,
+                bool store_u) {
+    fqlpop* h = c.h;
+    for (int l = 0; l < N.L; ++l) {
+        GemmArgs g{};
+        g.A = pref(h, h->params, N, N.W[l]);
+        g.B = l == 0 ? X : tref(G[l - 1], (long long)N.H * ldx * N.E, act_sy);
+        if (N.ln) {
+            g.C = tref(U[l], (long long)N.H * ldx * N.E, act_sy);
+        } else {
+            g.C = tref(store_u ? U[l] : G[l], (long long)N.H * ldx * N.E, act_sy);
+            g.C2 = tref(G[l], (long long)N.H * ldx * N.E, act_sy);
+        }
+        g.bias = pref(h, h->params, N, N.b[l]);
+        g.M = N.H; g.N = M; g.K = N.kdim(l);
+        g.lda = N.H; g.ldb = ldx; g.ldc = ldx;
+        g.ny = N.E; g.nz = c.nz; g.slots = h->slots;
+        const int epi = N.ln ? EPI_BIAS : (store_u ? EPI_BIAS_GELU2 : EPI_BIAS_GELU);
+        launch_gemm(LAYOUT_FWD, epi, pick_tile(g.M, g.N, g.ny * g.nz), g, s);
+        if (N.ln) {
+            LnArgs a{};
+            a.u = tref(U[l], (long long)N.H * ldx * N.E, act_sy);
+            a.h = tref(G[l], (long long)N.H * ldx * N.E, act_sy);
+            a.mu = tref((*MU)[l], (long long)ldx * N.E, st_sy);
+            a.rstd = tref((*RS)[l], (long long)ldx * N.E, st_sy);
+            a.gamma = pref(h, h->params, N, N.gam[l]);
+            a.beta = pref(h, h->params, N, N.bet[l]);
+            a.H = N.H; a.M = M; a.ld = ldx; a.ny = N.E; a.nz = c.nz; a.slots = h->slots;
+            launch_ln_gelu_fwd(a, s);
+        }
+    }
+}
+
+HeadArgs head_args(const Ctx& c, const NetLayout& N, float* Glast, int ldx, int M, long long act_sy) {
+    fqlpop* h = c.h;
+    HeadArgs a{};
+    a.h = tref(Glast, (long long)N.H * ldx * N.E, act_sy);
+    a.W = pref(h, h->params, N, N.W[N.L]);
+    a.b = pref(h, h->params, N, N.b[N.L]);
+    a.H = N.H; a.M = M; a.ld = ldx; a.nout = N.out_dim;
+    a.B = h->B; a.D = h->D;
+    a.steps_f = (float)h->S;
+    a.ny = N.E; a.nz = c.nz; a.slots = h->slots;
+    return a;
+}
+
+// Backward of one network from its head-output gradient `dout` ([nout][ld_o]).
+// Activations (U, G, X0) are read at column offset `coff` with leading dim
+// `ld`; M columns are back-propagated, of which the first Mg feed the
+// parameter gradients.
+void bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_o, TRef X0, int ld,
+             long long coff, int M, int Mg, const std::vector<float*>& U, const std::vector<float*>& G,
+             long long act_sy, const std::vector<float*>* MU, const std::vector<float*>* RS, long long st_sy,
+             const std::vector<float*>& DU, float* DH, float* C1, float* C2, int ld_d) {
+    fqlpop* h = c.h;
+    const long long act_ss = (long long)N.H * ld * N.E;
+    const long long d_ss = (long long)N.H * ld_d * N.E, d_sy = (long long)N.H * ld_d;
+    auto act = [&](float* p) { return tref(p + coff, act_ss, act_sy); };
+    for (int l = N.L - 1; l >= 0; --l) {
+        const bool head = (l == N.L - 1);
+        BwdArgs b{};
+        if (head) {
+            b.dout = dout;
+            b.W5 = pref(h, h->params, N, N.W[N.L]);
+            b.x_head = act(G[l]);
+            b.g_W5 = pref(h, h->grads, N, N.W[N.L]);
+        } else {
+            b.dh = tref(DH, d_ss, d_sy);
+        }
+        b.u = act(U[l]);
+        if (N.ln) {
+            b.mu = tref((*MU)[l] + coff, (long long)ld * N.E, st_sy);
+            b.rstd = tref((*RS)[l] + coff, (long long)ld * N.E, st_sy);
+            b.gamma = pref(h, h->params, N, N.gam[l]);
+            b.c1 = tref(C1, (long long)ld_d * N.E, ld_d);
+            b.c2 = tref(C2, (long long)ld_d * N.E, ld_d);
+            b.g_gamma = pref(h, h->grads, N, N.gam[l]);
+            b.g_beta = pref(h, h->grads, N, N.bet[l]);
+        }
+        b.du = tref(DU[l], d_ss, d_sy);
+        b.g_b = pref(h, h->grads, N, N.b[l]);
+        b.H = N.H; b.M = M; b.Mg = Mg; b.ld = ld; b.ld_d = ld_d; b.ld_o = ld_o; b.nout = N.out_dim;
+        b.ny = N.E; b.nz = c.nz; b.slots = h->slots;
+        if (N.ln) launch_bwd_rowstats(head, b, s);
+        launch_bwd_cols(head, N.ln, b, s);
+
+        // dW_l = X_l^T du_l over the first Mg columns
+        GemmArgs gw{};
+        gw.A = l == 0 ? X0 : act(G[l - 1]);
+        gw.B = tref(DU[l], d_ss, d_sy);
+        gw.C = pref(h, h->grads, N, N.W[l]);
+        gw.M = N.kdim(l); gw.N = N.H; gw.K = Mg;
+        gw.lda = ld; gw.ldb = ld_d; gw.ldc = N.H;
+        gw.ny = N.E; gw.nz = c.nz; gw.slots = h->slots;
+        launch_gemm(LAYOUT_DW, EPI_STORE, pick_tile(gw.M, gw.N, gw.ny * gw.nz), gw, s);
+        if (l > 0) {
+            // dh_{l-1} = W_l du_l  (all M columns)
+            GemmArgs gx{};
+            gx.A = pref(h, h->params, N, N.W[l]);
+            gx.B = tref(DU[l], d_ss, d_sy);
+            gx.C = tref(DH, d_ss, d_sy);
+            gx.M = N.H; gx.N = M; gx.K = N.H;
+            gx.lda = N.H; gx.ldb = ld_d; gx.ldc = ld_d;
+            gx.ny = N.E; gx.nz = c.nz; gx.slots = h->slots;
+            launch_gemm(LAYOUT_DX, EPI_STORE, pick_tile(gx.M, gx.N, gx.ny * gx.nz), gx, s);
+        }
+    }
+}
+
+void adam_net(const Ctx& c, hipStream_t s, int ni) {
+    fqlpop* h = c.h;
+    const NetLayout* nets[3] = {&h->critic, &h->bc, &h->os};
+    AdamArgs a{};
+    a.p = h->params; a.g = h->grads; a.m = h->adam_m; a.v = h->adam_v;
+    a.target = ni == 0 ? h->target : nullptr;
+    a.P = h->P; a.PT = h->PT;
+    a.net_off = nets[ni]->off;
+    a.chunks = h->chunks + h->chunk_base_net[ni];
+    a.n_chunks = h->n_chunks_net[ni];
+    a.chunk_base = h->chunk_base_net[ni];
+    a.stats = h->stats; a.n_total_chunks = h->n_chunks_total;
+    a.count = h->count;
+    a.lr = h->cfg.lr; a.tau = h->cfg.tau;
+    a.nz = c.nz; a.slots = h->slots;
+    launch_adam(a, s);
+}
+
+// Enqueue one population update (train) or one total_loss pass (!train).
+void enqueue(fqlpop* h, bool train, bool injected) {
+    const Ctx c{h, h->nz};
+    const int B = h->B, D = h->D, A = h->A, H = h->H, E = h->E, L = h->L, S = h->S;
+    const int Kc = D + A, Kb = D + A + 1;
+    const int B2 = 2 * B, B3 = 3 * B;
+    hipStream_t sM = h->sM, sF = h->sF, sB = h->sB;
+
+    // ---- sampling / assembly ------------------------------------------
+    const auto& dset = (!train && h->ds[1].rows > 0) ? h->ds[1] : h->ds[0];
+    SampleArgs sa{};
+    sa.obs = dset.obs; sa.act = dset.act; sa.rew = dset.rew; sa.mask = dset.mask; sa.nobs = dset.nobs;
+    sa.n_rows = dset.rows;
+    sa.inj_batch = injected ? h->inj_batch : nullptr;
+    sa.inj_noise = injected ? h->inj_noise : nullptr;
+    sa.seeds = h->seeds; sa.count = h->count;
+    sa.stream_salt = train ? 0x51A7u : 0x5A1Du;
+    sa.B = B; sa.D = D; sa.A = A;
+    sa.os_in = tref(h->os_in, (long long)Kc * B3);
+    sa.bc_in = tref(h->bc_in, (long long)Kb * B2);
+    sa.cr_in = tref(h->cr_in, (long long)Kc * B2);
+    sa.tg_in = tref(h->tg_in, (long long)Kc * B);
+    sa.eu_in = tref(h->eu_in, (long long)Kb * B);
+    sa.act_t = tref(h->act_t, (long long)A * B);
+    sa.x0_t = tref(h->x0_t, (long long)A * B);
+    sa.rew_t = tref(h->rew_t, B);
+    sa.mask_t = tref(h->mask_t, B);
+    sa.nz = c.nz; sa.slots = h->slots;
+    launch_sample(sa, sM);
+    HIPCHK(hipEventRecord(h->ev_sample, sM));
+    HIPCHK(hipStreamWaitEvent(sF, h->ev_sample, 0));
+    HIPCHK(hipStreamWaitEvent(sB, h->ev_sample, 0));
+
+    float* info = train ? h->info : h->vinfo;
+    LossArgs la{};
+    la.q = tref(h->q, (long long)E * B2, B2);
+    la.qt = tref(h->qt, (long long)E * B, B);
+    la.rew = tref(h->rew_t, B);
+    la.mask = tref(h->mask_t, B);
+    la.vpred = tref(h->vpred, (long long)A * B);
+    la.act = tref(h->act_t, (long long)A * B);
+    la.x0 = tref(h->x0_t, (long long)A * B);
+    la.amet = tref(h->amet, (long long)A * B);
+    la.apiraw = tref(h->apiraw, (long long)A * B);
+    la.aflow = tref(h->aflow, (long long)A * B);
+    la.da = tref(h->da, (long long)A * B);
+    la.dq = tref(h->dq, (long long)E * B2, B2);
+    la.dv = tref(h->dv, (long long)A * B);
+    la.dout_os = tref(h->dout_os, (long long)A * B);
+    la.g_cb4 = pref(h, h->grads, h->critic, h->critic.b[L]);
+    la.g_bcb4 = pref(h, h->grads, h->bc, h->bc.b[L]);
+    la.g_osb4 = pref(h, h->grads, h->os, h->os.b[L]);
+    la.info = tref(info, FQLPOP_INFO_STRIDE);
+    la.alpha = h->alpha;
+    la.B = B; la.A = A; la.E = E;
+    la.q_min = h->cfg.q_agg_min; la.normq = h->cfg.normalize_q_loss;
+    la.discount = h->cfg.discount;
+    la.nz = c.nz; la.slots = h->slots;
+
+    // ---- sF: BC-flow forward (train rows) fused with Euler step 0 --------
+    {
+        const NetLayout& N = h->bc;
+        fwd_hidden(c, sF, N, tref(h->bc_in, (long long)Kb * B2), B2, B2, h->bc_u, h->bc_g, 0,
+                   nullptr, nullptr, 0, true);
+        HeadArgs ha = head_args(c, N, h->bc_g[L - 1], B2, B2, 0);
+        ha.o0 = tref(h->vpred, (long long)A * B); ha.ld0 = B;
+        ha.o1 = tref(h->bc_in, (long long)Kb * B2); ha.ld1 = B2;
+        ha.o2 = tref(h->eu_in, (long long)Kb * B); ha.ld2 = B;
+        ha.t_next = (float)(1.0 / (double)S);
+        launch_head_fwd(HEAD_BC_FUSED, ha, sF);
+        HIPCHK(hipEventRecord(h->ev_bcfwd, sF));
+        for (int i = 1; i < S + (S == 1 ? 1 : 0); ++i) {
+            // S == 1: one zero-cost pass that only clips (not used by the configs here)
+            fwd_hidden(c, sF, N, tref(h->eu_in, (long long)Kb * B), B, B, h->eu_g, h->eu_g, 0,
+                       nullptr, nullptr, 0, false);
+            HeadArgs he = head_args(c, N, h->eu_g[L - 1], B, B, 0);
+            he.o0 = tref(h->aflow, (long long)A * B); he.ld0 = B;
+            he.o2 = tref(h->eu_in, (long long)Kb * B); he.ld2 = B;
+            he.last = (i == S - 1) ? 1 : 0;
+            he.t_next = (float)((double)(i + 1) / (double)S);
+            launch_head_fwd(HEAD_EULER, he, sF);
+        }
+        HIPCHK(hipEventRecord(h->ev_flow, sF));
+    }
+
+    // ---- sB: BC loss + backward (+ Adam after the flow chain) ------------
+    HIPCHK(hipStreamWaitEvent(sB, h->ev_bcfwd, 0));
+    launch_loss_bc(la, sB);
+    HIPCHK(hipEventRecord(h->ev_bcloss, sB));
+    if (train) {
+        const NetLayout& N = h->bc;
+        bwd_net(c, sB, N, tref(h->dv, (long long)A * B), B, tref(h->bc_in, (long long)Kb * B2), B2, 0, B, B,
+                h->bc_u, h->bc_g, 0, nullptr, nullptr, 0, h->bc_du, h->bc_dh, nullptr, nullptr, B);
+        HIPCHK(hipStreamWaitEvent(sB, h->ev_flow, 0));  // Euler reads bc params
+        adam_net(c, sB, 1);
+        HIPCHK(hipEventRecord(h->ev_bdone, sB));
+    }
+
+    // ---- sM: one-step actor forward on [s'; s; s] (z_next; z_d; z_metric) --
+    {
+        const NetLayout& N = h->os;
+        fwd_hidden(c, sM, N, tref(h->os_in, (long long)Kc * B3), B3, B3, h->os_u, h->os_g, 0,
+                   nullptr, nullptr, 0, true);
+        HeadArgs ha = head_args(c, N, h->os_g[L - 1], B3, B3, 0);
+        ha.o0 = tref(h->apiraw, (long long)A * B); ha.ld0 = B;
+        ha.o1 = tref(h->tg_in, (long long)Kc * B); ha.ld1 = B;
+        ha.o2 = tref(h->cr_in, (long long)Kc * B2); ha.ld2 = B2;
+        ha.o3 = tref(h->amet, (long long)A * B); ha.ld3 = B;
+        launch_head_fwd(HEAD_OS, ha, sM);
+    }
+    // ---- critic on [s,a ; s,clip(a_pi)] and target critic on [s', a'] ----
+    {
+        const NetLayout& N = h->critic;
+        const long long sy2 = (long long)H * B2, sy1 = (long long)H * B;
+        fwd_hidden(c, sM, N, tref(h->cr_in, (long long)Kc * B2, 0), B2, B2, h->cr_u, h->cr_h, sy2,
+                   &h->cr_mu, &h->cr_rs, B2, true);
+        HeadArgs hc = head_args(c, N, h->cr_h[L - 1], B2, B2, sy2);
+        hc.o0 = tref(h->q, (long long)E * B2, B2); hc.ld0 = B2;
+        launch_head_fwd(HEAD_STORE, hc, sM);
+
+        // target critic: same layout, params from the target arena
+        for (int l = 0; l < L; ++l) {
+            GemmArgs g{};
+            g.A = tref(h->target + N.W[l], h->PT, N.ens_size);
+            g.B = l == 0 ? tref(h->tg_in, (long long)Kc * B, 0) : tref(h->tg_h[l - 1], (long long)H * B * E, sy1);
+            g.C = tref(N.ln ? h->tg_u[l] : h->tg_h[l], (long long)H * B * E, sy1);
+            g.bias = tref(h->target + N.b[l], h->PT, N.ens_size);
+            g.M = H; g.N = B; g.K = N.kdim(l);
+            g.lda = H; g.ldb = B; g.ldc = B;
+            g.ny = E; g.nz = c.nz; g.slots = h->slots;
+            launch_gemm(LAYOUT_FWD, N.ln ? EPI_BIAS : EPI_BIAS_GELU, pick_tile(g.M, g.N, g.ny * g.nz), g, sM);
+            if (N.ln) {
+                LnArgs a{};
+                a.u = tref(h->tg_u[l], (long long)H * B * E, sy1);
+                a.h = tref(h->tg_h[l], (long long)H * B * E, sy1);
+                a.mu = tref(h->tg_mu[l], (long long)B * E, B);
+                a.rstd = tref(h->tg_rs[l], (long long)B * E, B);
+                a.gamma = tref(h->target + N.gam[l], h->PT, N.ens_size);
+                a.beta = tref(h->target + N.bet[l], h->PT, N.ens_size);
+                a.H = H; a.M = B; a.ld = B; a.ny = E; a.nz = c.nz; a.slots = h->slots;
+                launch_ln_gelu_fwd(a, sM);
+            }
+        }
+        HeadArgs ht{};
+        ht.h = tref(h->tg_h[L - 1], (long long)H * B * E, sy1);
+        ht.W = tref(h->target + N.W[L], h->PT, N.ens_size);
+        ht.b = tref(h->target + N.b[L], h->PT, N.ens_size);
+        ht.H = H; ht.M = B; ht.ld = B; ht.nout = 1; ht.B = B; ht.D = D; ht.steps_f = (float)S;
+        ht.o0 = tref(h->qt, (long long)E * B, B); ht.ld0 = B;
+        ht.ny = E; ht.nz = c.nz; ht.slots = h->slots;
+        launch_head_fwd(HEAD_STORE, ht, sM);
+    }
+    launch_loss_critic(la, sM);
+    if (train) {
+        const NetLayout& N = h->critic;
+        const long long sy2 = (long long)H * B2;
+        bwd_net(c, sM, N, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0), B2, 0,
+                B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, h->cr_dh, h->cr_c1, h->cr_c2, B2);
+        InGradArgs ig{};
+        ig.W0 = pref(h, h->params, N, N.W[0]);
+        ig.du0 = tref(h->cr_du[0], (long long)H * B2 * E, sy2);
+        ig.da = tref(h->da, (long long)A * B);
+        ig.H = H; ig.D = D; ig.A = A; ig.E = E; ig.ld = B2; ig.off = B; ig.M = B;
+        ig.nz = c.nz; ig.slots = h->slots;
+        launch_input_grad(ig, sM);
+        adam_net(c, sM, 0);  // critic Adam + target EMA (all critic reads of this step are done)
+    }
+    HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
+    HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
+    launch_loss_actor(la, sM);
+    if (train) {
+        const NetLayout& N = h->os;
+        bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3, B, B, B,
+                h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, h->os_dh, nullptr, nullptr, B);
+        adam_net(c, sM, 2);
+        HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
+        FinalArgs fa{};
+        fa.stats = h->stats; fa.chunk_leaf = h->chunk_leaf;
+        fa.n_total_chunks = h->n_chunks_total; fa.n_leaves = h->n_train_leaves;
+        fa.info = tref(h->info, FQLPOP_INFO_STRIDE);
+        fa.count = h->count;
+        fa.nz = c.nz; fa.slots = h->slots;
+        launch_finalize(fa, sM);
+    } else {
+        HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
+    }
+    HIPCHK(hipGetLastError());
+}
+
+void run(fqlpop* h, bool train, bool injected) {
+    if (h->nz == 0) return;
+    if (!h->cfg.use_graph) {
+        enqueue(h, train, injected);
+        return;
+    }
+    const int key = (train ? 2 : 0) + (injected ? 1 : 0);
+    Graphs& gr = h->graphs[key];
+    if (gr.exec == nullptr || gr.nz != h->nz) {
+        if (gr.exec) HIPCHK(hipGraphExecDestroy(gr.exec));
+        gr.exec = nullptr;
+        hipGraph_t graph;
+        HIPCHK(hipStreamBeginCapture(h->sM, hipStreamCaptureModeRelaxed));
+        try {
+            enqueue(h, train, injected);
+        } catch (...) {
+            (void)hipStreamEndCapture(h->sM, &graph);
+            throw;
+        }
+        HIPCHK(hipStreamEndCapture(h->sM, &graph));
+        HIPCHK(hipGraphInstantiate(&gr.exec, graph, nullptr, nullptr, 0));
+        HIPCHK(hipGraphDestroy(graph));
+        gr.nz = h->nz;
+    }
+    HIPCHK(hipGraphLaunch(gr.exec, h->sM));
+}
+
+void update_slots(fqlpop* h) {
+    h->h_slots.clear();
+    for (int i = 0; i < h->n; ++i)
+        if (h->active[i]) h->h_slots.push_back(i);
+    h->nz = (int)h->h_slots.size();
+    HIPCHK(hipStreamSynchronize(h->sM));
+    if (h->nz) HIPCHK(hipMemcpy(h->slots, h->h_slots.data(), sizeof(int) * h->nz, hipMemcpyHostToDevice));
+}
+
+template <typename F>
+int guard(F&& f) {
+    try {
+        f();
+        g_err.clear();
+        return FQLPOP_OK;
+    } catch (const FqErr& e) {
+        g_err = e.msg;
+        return e.code;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return FQLPOP_E_STATE;
+    }
+}
+
+void check_member(fqlpop* h, int member) {
+    ARGCHK(h != nullptr, "null handle");
+    ARGCHK(member >= 0 && member < h->n, "member index out of range");
+}
+
+}  // namespace
+
+// =================================================================== C ABI ==
+extern "C" {
+
+const char* fqlpop_last_error(void) { return g_err.c_str(); }
+
+double fqlpop_flops_per_member_step(const fqlpop_config* c) {
+    // F(i,o) = 2B(iH + (L-1)H^2 + Ho) per forward; dX without
+    // the first layer = 2B((L-1)H^2 + Ho).
+    const double B = c->batch_size, H = c->hidden_dim, L = c->num_hidden, D = c->obs_dim, A = c->action_dim;
+    const double E = c->num_qs, S = c->flow_steps;
+    auto F = [&](double i, double o) { return 2.0 * B * (i * H + (L - 1) * H * H + H * o); };
+    auto dX = [&](double o) { return 2.0 * B * ((L - 1) * H * H + H * o); };
+    const double Fc = F(D + A, 1), Fbc = F(D + A + 1, A), Fos = F(D + A, A);
+    return Fos + E * Fc + E * Fc + E * Fc + E * dX(1) + Fbc + Fbc + dX(A) + S * Fbc + Fos + Fos + dX(A) +
+           E * Fc + E * Fc + Fos;
+}
+
+int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, const uint64_t* seeds_in,
+                  int device, fqlpop_t** out) {
+    return guard([&] {
+        ARGCHK(cfg && out && alphas && seeds_in, "null argument");
+        ARGCHK(n_members > 0, "n_members must be > 0");
+        ARGCHK(cfg->action_dim >= 1 && cfg->action_dim <= 8, "action_dim must be in [1, 8]");
+        ARGCHK(cfg->obs_dim >= 1, "obs_dim must be >= 1");
+        ARGCHK(cfg->hidden_dim >= 64 && cfg->hidden_dim % 64 == 0, "hidden_dim must be a multiple of 64");
+        ARGCHK(cfg->num_hidden >= 1, "num_hidden must be >= 1");
+        ARGCHK(cfg->batch_size >= 64 && cfg->batch_size % 64 == 0, "batch_size must be a multiple of 64");
+        ARGCHK(cfg->num_qs >= 1 && cfg->num_qs <= 4, "num_qs must be in [1, 4]");
+        ARGCHK(cfg->flow_steps >= 2, "flow_steps must be >= 2");
+        auto h = std::make_unique<fqlpop>();
+        h->cfg = *cfg;
+        h->n = n_members;
+        h->device = device;
+        HIPCHK(hipSetDevice(device));
+        h->D = cfg->obs_dim; h->A = cfg->action_dim; h->H = cfg->hidden_dim; h->L = cfg->num_hidden;
+        h->B = cfg->batch_size; h->E = cfg->num_qs; h->S = cfg->flow_steps;
+        const int D = h->D, A = h->A, H = h->H, L = h->L, B = h->B, E = h->E;
+        h->critic.build("critic", D + A, 1, L, H, E, cfg->layer_norm != 0);
+        h->bc.build("actor_bc_flow", D + A + 1, A, L, H, 1, cfg->actor_layer_norm != 0);
+        h->os.build("actor_onestep_flow", D + A, A, L, H, 1, cfg->actor_layer_norm != 0);
+        h->critic.off = 0;
+        h->bc.off = align_up(h->critic.size());
+        h->os.off = align_up(h->bc.off + h->bc.size());
+        h->P = align_up(h->os.off + h->os.size());
+        h->PT = align_up(h->critic.size());
+        build_leaves(h.get());
+
+        HIPCHK(hipStreamCreateWithFlags(&h->sM, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&h->sF, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
+        for (hipEvent_t* e : {&h->ev_sample, &h->ev_bcfwd, &h->ev_bcloss, &h->ev_flow, &h->ev_bdone})
+            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        HIPCHK(hipEventCreate(&h->ev_t0));
+        HIPCHK(hipEventCreate(&h->ev_t1));
+
+        const int n = h->n;
+        HIPCHK(hipMalloc(&h->params, sizeof(float) * h->P * n));
+        HIPCHK(hipMalloc(&h->grads, sizeof(float) * h->P * n));
+        HIPCHK(hipMalloc(&h->adam_m, sizeof(float) * h->P * n));
+        HIPCHK(hipMalloc(&h->adam_v, sizeof(float) * h->P * n));
+        HIPCHK(hipMalloc(&h->target, sizeof(float) * h->PT * n));
+        HIPCHK(hipMemset(h->params, 0, sizeof(float) * h->P * n));
+        HIPCHK(hipMemset(h->grads, 0, sizeof(float) * h->P * n));
+        HIPCHK(hipMalloc(&h->count, sizeof(int) * n));
+        HIPCHK(hipMalloc(&h->seeds, sizeof(uint64_t) * n));
+        HIPCHK(hipMalloc(&h->alpha, sizeof(float) * n));
+        HIPCHK(hipMalloc(&h->slots, sizeof(int) * n));
+        build_chunks(h.get());
+
+        const int Kc = D + A, Kb = D + A + 1, B2 = 2 * B, B3 = 3 * B;
+        h->os_in = h->alloc(align_up((long long)Kc * B3));
+        h->bc_in = h->alloc(align_up((long long)Kb * B2));
+        h->eu_in = h->alloc(align_up((long long)Kb * B));
+        h->cr_in = h->alloc(align_up((long long)Kc * B2));
+        h->tg_in = h->alloc(align_up((long long)Kc * B));
+        for (int l = 0; l < L; ++l) {
+            h->os_u.push_back(h->alloc((long long)H * B3));
+            h->os_g.push_back(h->alloc((long long)H * B3));
+            h->bc_u.push_back(h->alloc((long long)H * B2));
+            h->bc_g.push_back(h->alloc((long long)H * B2));
+            h->eu_g.push_back(h->alloc((long long)H * B));
+            h->cr_u.push_back(h->alloc((long long)H * B2 * E));
+            h->cr_h.push_back(h->alloc((long long)H * B2 * E));
+            h->cr_mu.push_back(h->alloc((long long)B2 * E));
+            h->cr_rs.push_back(h->alloc((long long)B2 * E));
+            h->tg_u.push_back(h->alloc((long long)H * B * E));
+            h->tg_h.push_back(h->alloc((long long)H * B * E));
+            h->tg_mu.push_back(h->alloc((long long)B * E));
+            h->tg_rs.push_back(h->alloc((long long)B * E));
+            h->cr_du.push_back(h->alloc((long long)H * B2 * E));
+            h->bc_du.push_back(h->alloc((long long)H * B));
+            h->os_du.push_back(h->alloc((long long)H * B));
+        }
+        h->cr_dh = h->alloc((long long)H * B2 * E);
+        h->bc_dh = h->alloc((long long)H * B);
+        h->os_dh = h->alloc((long long)H * B);
+        h->cr_c1 = h->alloc((long long)B2 * E);
+        h->cr_c2 = h->alloc((long long)B2 * E);
+        h->q = h->alloc((long long)E * B2);
+        h->dq = h->alloc((long long)E * B2);
+        h->qt = h->alloc((long long)E * B);
+        for (float** p : {&h->vpred, &h->dv, &h->act_t, &h->x0_t, &h->apiraw, &h->aflow, &h->amet, &h->da,
+                          &h->dout_os})
+            *p = h->alloc((long long)A * B);
+        h->rew_t = h->alloc(B);
+        h->mask_t = h->alloc(B);
+        h->info = h->alloc(FQLPOP_INFO_STRIDE);
+        h->vinfo = h->alloc(FQLPOP_INFO_STRIDE);
+        h->inj_bs = (long long)B * (2 * D + A + 2);
+        h->inj_ns = (long long)B * (4 * A + 1);
+        h->inj_batch = h->alloc(h->inj_bs);
+        h->inj_noise = h->alloc(h->inj_ns);
+
+        h->h_alpha.assign(alphas, alphas + n);
+        h->h_seeds.assign(seeds_in, seeds_in + n);
+        HIPCHK(hipMemcpy(h->alpha, alphas, sizeof(float) * n, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(h->seeds, seeds_in, sizeof(uint64_t) * n, hipMemcpyHostToDevice));
+        for (int i = 0; i < n; ++i) init_member(h.get(), i, seeds_in[i]);
+        h->active.assign(n, 1);
+        update_slots(h.get());
+        HIPCHK(hipDeviceSynchronize());
+        *out = h.release();
+    });
+}
+
+int fqlpop_destroy(fqlpop_t* h) {
+    return guard([&] {
+        if (!h) return;
+        (void)hipSetDevice(h->device);
+        (void)hipDeviceSynchronize();
+        for (auto& kv : h->graphs)
+            if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+        for (float* p : h->allocs) (void)hipFree(p);
+        for (void* p : {(void*)h->params, (void*)h->grads, (void*)h->adam_m, (void*)h->adam_v, (void*)h->target,
+                        (void*)h->count, (void*)h->seeds, (void*)h->alpha, (void*)h->slots, (void*)h->stats,
+                        (void*)h->chunks, (void*)h->chunk_leaf})
+            if (p) (void)hipFree(p);
+        for (auto& d : h->ds)
+            for (float* p : {d.obs, d.act, d.rew, d.mask, d.nobs})
+                if (p) (void)hipFree(p);
+        for (hipEvent_t e : {h->ev_sample, h->ev_bcfwd, h->ev_bcloss, h->ev_flow, h->ev_bdone, h->ev_t0, h->ev_t1})
+            if (e) (void)hipEventDestroy(e);
+        for (hipStream_t s : {h->sM, h->sF, h->sB})
+            if (s) (void)hipStreamDestroy(s);
+        delete h;
+    });
+}
+
+int fqlpop_set_dataset(fqlpop_t* h, int which, const float* obs, const float* act, const float* rew,
+                       const float* mask, const float* next_obs, int64_t n_rows, int on_device) {
+    return guard([&] {
+        ARGCHK(h && obs && act && rew && mask && next_obs, "null argument");
+        ARGCHK(which == 0 || which == 1, "which must be 0 (train) or 1 (val)");
+        ARGCHK(n_rows > 0 && n_rows < (1LL << 32), "n_rows out of range");
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        auto& d = h->ds[which];
+        for (float* p : {d.obs, d.act, d.rew, d.mask, d.nobs})
+            if (p) HIPCHK(hipFree(p));
+        const long long n = n_rows;
+        const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+        auto up = [&](float** dst, const float* src, long long cnt) {
+            HIPCHK(hipMalloc(dst, sizeof(float) * cnt));
+            HIPCHK(hipMemcpy(*dst, src, sizeof(float) * cnt, kind));
+        };
+        up(&d.obs, obs, n * h->D);
+        up(&d.act, act, n * h->A);
+        up(&d.rew, rew, n);
+        up(&d.mask, mask, n);
+        up(&d.nobs, next_obs, n * h->D);
+        d.rows = n;
+        // graphs bake dataset pointers in: drop them
+        for (auto& kv : h->graphs)
+            if (kv.second.exec) { HIPCHK(hipGraphExecDestroy(kv.second.exec)); kv.second.exec = nullptr; }
+    });
+}
+
+int fqlpop_set_active(fqlpop_t* h, const uint8_t* mask) {
+    return guard([&] {
+        ARGCHK(h && mask, "null argument");
+        for (int i = 0; i < h->n; ++i) h->active[i] = mask[i] ? 1 : 0;
+        update_slots(h);
+    });
+}
+
+int fqlpop_step(fqlpop_t* h, int n_steps) {
+    return guard([&] {
+        ARGCHK(h, "null handle");
+        ARGCHK(n_steps >= 0, "n_steps must be >= 0");
+        if (h->ds[0].rows == 0) throw FqErr{FQLPOP_E_STATE, "no training dataset set (fqlpop_set_dataset)"};
+        HIPCHK(hipSetDevice(h->device));
+        for (int i = 0; i < n_steps; ++i) run(h, true, false);
+    });
+}
+
+int fqlpop_step_injected(fqlpop_t* h, const float* batch, const float* noise) {
+    return guard([&] {
+        ARGCHK(h && batch && noise, "null argument");
+        HIPCHK(hipSetDevice(h->device));
+        if (h->nz == 0) return;
+        HIPCHK(hipMemcpyAsync(h->inj_batch, batch, sizeof(float) * h->inj_bs * h->nz, hipMemcpyHostToDevice, h->sM));
+        HIPCHK(hipMemcpyAsync(h->inj_noise, noise, sizeof(float) * h->inj_ns * h->nz, hipMemcpyHostToDevice, h->sM));
+        run(h, true, true);
+        HIPCHK(hipStreamSynchronize(h->sM));  // host buffers are borrowed only for the call
+    });
+}
+
+int fqlpop_total_loss(fqlpop_t* h, const float* batch, const float* noise) {
+    return guard([&] {
+        ARGCHK(h, "null handle");
+        ARGCHK((batch == nullptr) == (noise == nullptr), "batch and noise must both be given or both NULL");
+        HIPCHK(hipSetDevice(h->device));
+        if (h->nz == 0) return;
+        const bool inj = batch != nullptr;
+        if (!inj && h->ds[0].rows == 0 && h->ds[1].rows == 0)
+            throw FqErr{FQLPOP_E_STATE, "no dataset set"};
+        if (inj) {
+            HIPCHK(hipMemcpyAsync(h->inj_batch, batch, sizeof(float) * h->inj_bs * h->nz, hipMemcpyHostToDevice, h->sM));
+            HIPCHK(hipMemcpyAsync(h->inj_noise, noise, sizeof(float) * h->inj_ns * h->nz, hipMemcpyHostToDevice, h->sM));
+        }
+        run(h, false, inj);
+        if (inj) HIPCHK(hipStreamSynchronize(h->sM));
+    });
+}
+
+int fqlpop_read_info(fqlpop_t* h, int which, float* out) {
+    return guard([&] {
+        ARGCHK(h && out, "null argument");
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipStreamSynchronize(h->sM));
+        HIPCHK(hipMemcpy(out, which ? h->vinfo : h->info, sizeof(float) * FQLPOP_INFO_STRIDE * h->n,
+                         hipMemcpyDeviceToHost));
+    });
+}
+
+int fqlpop_sample_actions(fqlpop_t* h, int member, const float* obs, int64_t n, const float* noise, uint64_t seed,
+                          float* out) {
+    return guard([&] {
+        check_member(h, member);
+        ARGCHK(obs && out && n > 0, "bad argument");
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipStreamSynchronize(h->sM));
+        const int D = h->D, A = h->A, H = h->H, L = h->L, Kc = D + A;
+        const long long M = (n + 63) / 64 * 64;
+        // feature-major input [s; z] built on the host
+        std::vector<float> x((size_t)Kc * M, 0.f);
+        for (long long r = 0; r < n; ++r) {
+            for (int k = 0; k < D; ++k) x[(size_t)k * M + r] = obs[r * D + k];
+            for (int j = 0; j < A; j += 2) {
+                float z0, z1;
+                if (noise) {
+                    z0 = noise[r * A + j];
+                    z1 = (j + 1 < A) ? noise[r * A + j + 1] : 0.f;
+                } else {
+                    uint32_t c[4] = {(uint32_t)r, (uint32_t)(r >> 32), 0xAC7u, (uint32_t)j};
+                    philox_host(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+                    const float u1 = ((c[0] >> 8) + 1u) * (1.0f / 16777216.0f);
+                    const float u2 = (c[1] >> 8) * (1.0f / 16777216.0f);
+                    const float rr = std::sqrt(-2.0f * std::log(u1));
+                    z0 = rr * std::cos(6.283185307179586f * u2);
+                    z1 = rr * std::sin(6.283185307179586f * u2);
+                }
+                x[(size_t)(D + j) * M + r] = z0;
+                if (j + 1 < A) x[(size_t)(D + j + 1) * M + r] = z1;
+            }
+        }
+        float *dx = nullptr, *dout = nullptr, *dg = nullptr;
+        int* dslot = nullptr;
+        HIPCHK(hipMalloc(&dx, sizeof(float) * x.size()));
+        HIPCHK(hipMalloc(&dout, sizeof(float) * A * M));
+        HIPCHK(hipMalloc(&dg, sizeof(float) * 2 * H * M));
+        HIPCHK(hipMalloc(&dslot, sizeof(int)));
+        HIPCHK(hipMemcpy(dx, x.data(), sizeof(float) * x.size(), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dslot, &member, sizeof(int), hipMemcpyHostToDevice));
+        const NetLayout& N = h->os;
+        float* buf[2] = {dg, dg + (long long)H * M};
+        for (int l = 0; l < L; ++l) {
+            GemmArgs g{};
+            g.A = tref(h->params + N.off + N.W[l], h->P);
+            g.B = l == 0 ? tref(dx, 0) : tref(buf[(l - 1) & 1], 0);
+            g.C = tref(buf[l & 1], 0);
+            g.bias = tref(h->params + N.off + N.b[l], h->P);
+            g.M = H; g.N = (int)M; g.K = N.kdim(l);
+            g.lda = H; g.ldb = (int)M; g.ldc = (int)M;
+            g.ny = 1; g.nz = 1; g.slots = dslot;
+            if (N.ln) {
+                throw FqErr{FQLPOP_E_UNSUPPORTED, "sample_actions with actor_layer_norm is not supported"};
+            }
+            launch_gemm(LAYOUT_FWD, EPI_BIAS_GELU, 0, g, h->sM);
+        }
+        HeadArgs ha{};
+        ha.h = tref(buf[(L - 1) & 1], 0);
+        ha.W = tref(h->params + N.off + N.W[L], h->P);
+        ha.b = tref(h->params + N.off + N.b[L], h->P);
+        ha.H = H; ha.M = (int)M; ha.ld = (int)M; ha.nout = A; ha.B = h->B; ha.D = D; ha.steps_f = 1.f;
+        ha.o0 = tref(dout, 0); ha.ld0 = (int)M;
+        ha.ny = 1; ha.nz = 1; ha.slots = dslot;
+        launch_head_fwd(HEAD_ACT, ha, h->sM);
+        HIPCHK(hipGetLastError());
+        std::vector<float> o((size_t)A * M);
+        HIPCHK(hipStreamSynchronize(h->sM));
+        HIPCHK(hipMemcpy(o.data(), dout, sizeof(float) * o.size(), hipMemcpyDeviceToHost));
+        for (long long r = 0; r < n; ++r)
+            for (int j = 0; j < A; ++j) out[r * A + j] = o[(size_t)j * M + r];
+        (void)hipFree(dx); (void)hipFree(dout); (void)hipFree(dg); (void)hipFree(dslot);
+    });
+}
+
+int fqlpop_state_size(fqlpop_t* h, int64_t* n_floats) {
+    return guard([&] {
+        ARGCHK(h && n_floats, "null argument");
+        *n_floats = h->state_size;
+    });
+}
+
+static void state_copy(fqlpop* h, int member, int which, float* flat, const float* in, bool get) {
+    ARGCHK(which >= 0 && which <= 2, "which must be FQLPOP_STATE_PARAMS/ADAM_M/ADAM_V");
+    float* arena = which == 0 ? h->params : which == 1 ? h->adam_m : h->adam_v;
+    std::vector<float> blk((size_t)h->P), tblk((size_t)h->PT, 0.f);
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(blk.data(), arena + (long long)member * h->P, sizeof(float) * h->P, hipMemcpyDeviceToHost));
+    if (which == 0)
+        HIPCHK(hipMemcpy(tblk.data(), h->target + (long long)member * h->PT, sizeof(float) * h->PT,
+                         hipMemcpyDeviceToHost));
+    for (const Leaf& lf : h->leaves) {
+        const NetLayout& N = lf.net == 2 ? h->bc : lf.net == 3 ? h->os : h->critic;
+        const bool is_target = lf.net == 1;
+        float* src = is_target ? tblk.data() : blk.data() + N.off;
+        const long long per = leaf_member_size(N, lf.kind, lf.layer);
+        for (int e = 0; e < N.E; ++e) {
+            float* p = src + e * N.ens_size + leaf_internal_off(N, lf.kind, lf.layer);
+            const long long fo = lf.flat_off + e * per;
+            if (get) {
+                if (is_target && which != 0) std::fill(flat + fo, flat + fo + per, 0.f);
+                else std::memcpy(flat + fo, p, sizeof(float) * per);
+            } else {
+                std::memcpy(p, in + fo, sizeof(float) * per);
+            }
+        }
+    }
+    if (!get) {
+        HIPCHK(hipMemcpy(arena + (long long)member * h->P, blk.data(), sizeof(float) * h->P, hipMemcpyHostToDevice));
+        if (which == 0)
+            HIPCHK(hipMemcpy(h->target + (long long)member * h->PT, tblk.data(), sizeof(float) * h->PT,
+                             hipMemcpyHostToDevice));
+    }
+}
+
+int fqlpop_get_state(fqlpop_t* h, int member, int which, float* flat, int64_t n) {
+    return guard([&] {
+        check_member(h, member);
+        ARGCHK(flat && n == h->state_size, "flat buffer size mismatch");
+        state_copy(h, member, which, flat, nullptr, true);
+    });
+}
+
+int fqlpop_set_state(fqlpop_t* h, int member, int which, const float* flat, int64_t n) {
+    return guard([&] {
+        check_member(h, member);
+        ARGCHK(flat && n == h->state_size, "flat buffer size mismatch");
+        state_copy(h, member, which, nullptr, flat, false);
+    });
+}
+
+int fqlpop_get_count(fqlpop_t* h, int member, int32_t* count) {
+    return guard([&] {
+        check_member(h, member);
+        ARGCHK(count, "null argument");
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy(count, h->count + member, sizeof(int), hipMemcpyDeviceToHost));
+    });
+}
+
+int fqlpop_set_count(fqlpop_t* h, int member, int32_t count) {
+    return guard([&] {
+        check_member(h, member);
+        ARGCHK(count >= 0, "count must be >= 0");
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy(h->count + member, &count, sizeof(int), hipMemcpyHostToDevice));
+    });
+}
+
+int fqlpop_set_member(fqlpop_t* h, int member, float alpha, uint64_t seed, int reinit) {
+    return guard([&] {
+        check_member(h, member);
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        h->h_alpha[member] = alpha;
+        h->h_seeds[member] = seed;
+        HIPCHK(hipMemcpy(h->alpha + member, &alpha, sizeof(float), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(h->seeds + member, &seed, sizeof(uint64_t), hipMemcpyHostToDevice));
+        if (reinit) init_member(h, member, seed);
+    });
+}
+
+int fqlpop_num_leaves(fqlpop_t* h, int* n) {
+    return guard([&] {
+        ARGCHK(h && n, "null argument");
+        *n = (int)h->leaves.size();
+    });
+}
+
+int fqlpop_leaf_info(fqlpop_t* h, int i, char* name, int name_cap, int64_t* offset, int* ndim, int64_t* shape3) {
+    return guard([&] {
+        ARGCHK(h && name && offset && ndim && shape3 && name_cap > 0, "null argument");
+        ARGCHK(i >= 0 && i < (int)h->leaves.size(), "leaf index out of range");
+        const Leaf& lf = h->leaves[i];
+        std::snprintf(name, name_cap, "%s", lf.name.c_str());
+        *offset = lf.flat_off;
+        *ndim = lf.ndim;
+        for (int k = 0; k < 3; ++k) shape3[k] = k < lf.ndim ? lf.shape[k] : 0;
+    });
+}
+
+int fqlpop_sync(fqlpop_t* h) {
+    return guard([&] {
+        ARGCHK(h, "null handle");
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipStreamSynchronize(h->sM));
+        HIPCHK(hipStreamSynchronize(h->sF));
+        HIPCHK(hipStreamSynchronize(h->sB));
+    });
+}
+
+int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* flops) {
+    return guard([&] {
+        ARGCHK(h && avg_us && flops && iters > 0, "bad argument");
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        const NetLayout& N = h->bc;
+        const int B = h->B, H = h->H;
+        // Euler hidden layer 1: eu_g[1] = gelu(W1^T eu_g[0] + b1), all active members
+        GemmArgs g{};
+        g.A = pref(h, h->params, N, N.W[1]);
+        g.B = tref(h->eu_g[0], (long long)H * B);
+        g.C = tref(h->eu_g[1], (long long)H * B);
+        g.bias = pref(h, h->params, N, N.b[1]);
+        g.M = H; g.N = B; g.K = H; g.lda = H; g.ldb = B; g.ldc = B;
+        g.ny = 1; g.nz = h->nz; g.slots = h->slots;
+        const int tile = pick_tile(g.M, g.N, g.nz);
+        launch_gemm(LAYOUT_FWD, EPI_BIAS_GELU, tile, g, h->sF);  // warm-up
+        HIPCHK(hipEventRecord(h->ev_t0, h->sF));
+        for (int i = 0; i < iters; ++i) launch_gemm(LAYOUT_FWD, EPI_BIAS_GELU, tile, g, h->sF);
+        HIPCHK(hipEventRecord(h->ev_t1, h->sF));
+        HIPCHK(hipEventSynchronize(h->ev_t1));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, h->ev_t0, h->ev_t1));
+        *avg_us = 1000.0 * ms / iters;
+        *flops = 2.0 * H * (double)B * H * h->nz;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,8 @@
+"""fqlpop -- MI355X-native Flow Q-Learning population trainer (HIP kernels behind a C ABI).
+
+``Population`` is the engine; ``fql.agents.fql.FQLAgent`` and ``trainer.Trainer``
+(sibling packages) keep the reference's surface on top of it.
+"""
+from fqlpop._lib import (EXPORTED_SYMBOLS, LIB_PATH, TRAIN_INFO_KEYS, VAL_INFO_KEYS,  # noqa: F401
+                         FqlpopError, load_library)
+from fqlpop.population import Population, PopulationConfig  # noqa: F401

@@ -1,0 +1,119 @@
+"""ctypes binding of libfqlpop.so (the C ABI in include/fqlpop.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (``make -C
+flow-q-learning_amd/csrc``) and loaded from this directory.  There is no
+fallback: if the library is missing or fails to load, every entry point raises.
+``torch`` is imported first when available so that the process has ONE HIP
+runtime (torch's bundled libamdhip64.so.7 and ROCm's share the soname).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+try:  # share torch's HIP runtime if torch is around (it usually is)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is in the image
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfqlpop.so")
+
+INFO_STRIDE = 16
+TRAIN_INFO_KEYS = (
+    "critic/critic_loss", "critic/q_mean", "critic/q_max", "critic/q_min",
+    "actor/actor_loss", "actor/bc_flow_loss", "actor/distill_loss",
+    "actor/q_loss", "actor/q", "actor/mse",
+    "grad/max", "grad/min", "grad/norm",
+)
+VAL_INFO_KEYS = TRAIN_INFO_KEYS[:10]
+STATE_PARAMS, STATE_ADAM_M, STATE_ADAM_V = 0, 1, 2
+
+
+class FqlpopError(RuntimeError):
+    pass
+
+
+class Config(ctypes.Structure):
+    """Mirror of ``fqlpop_config`` (include/fqlpop.h)."""
+    _fields_ = [
+        ("obs_dim", ctypes.c_int), ("action_dim", ctypes.c_int),
+        ("hidden_dim", ctypes.c_int), ("num_hidden", ctypes.c_int),
+        ("batch_size", ctypes.c_int), ("num_qs", ctypes.c_int),
+        ("layer_norm", ctypes.c_int), ("actor_layer_norm", ctypes.c_int),
+        ("flow_steps", ctypes.c_int), ("q_agg_min", ctypes.c_int),
+        ("normalize_q_loss", ctypes.c_int),
+        ("discount", ctypes.c_float), ("tau", ctypes.c_float), ("lr", ctypes.c_float),
+        ("use_graph", ctypes.c_int),
+    ]
+
+
+_P = ctypes.c_void_p
+_F = ctypes.POINTER(ctypes.c_float)
+_SIGS = {
+    "fqlpop_last_error": (ctypes.c_char_p, []),
+    "fqlpop_create": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.c_int, _F,
+                                     ctypes.POINTER(ctypes.c_uint64), ctypes.c_int,
+                                     ctypes.POINTER(_P)]),
+    "fqlpop_destroy": (ctypes.c_int, [_P]),
+    "fqlpop_set_dataset": (ctypes.c_int, [_P, ctypes.c_int, _P, _P, _P, _P, _P,
+                                          ctypes.c_int64, ctypes.c_int]),
+    "fqlpop_set_active": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint8)]),
+    "fqlpop_step": (ctypes.c_int, [_P, ctypes.c_int]),
+    "fqlpop_step_injected": (ctypes.c_int, [_P, _F, _F]),
+    "fqlpop_total_loss": (ctypes.c_int, [_P, _F, _F]),
+    "fqlpop_read_info": (ctypes.c_int, [_P, ctypes.c_int, _F]),
+    "fqlpop_sample_actions": (ctypes.c_int, [_P, ctypes.c_int, _F, ctypes.c_int64, _F,
+                                             ctypes.c_uint64, _F]),
+    "fqlpop_state_size": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
+    "fqlpop_get_state": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _F, ctypes.c_int64]),
+    "fqlpop_set_state": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _F, ctypes.c_int64]),
+    "fqlpop_get_count": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]),
+    "fqlpop_set_count": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int32]),
+    "fqlpop_set_member": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_float, ctypes.c_uint64,
+                                         ctypes.c_int]),
+    "fqlpop_num_leaves": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int)]),
+    "fqlpop_leaf_info": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_int),
+                                        ctypes.POINTER(ctypes.c_int64)]),
+    "fqlpop_sync": (ctypes.c_int, [_P]),
+    "fqlpop_time_dominant_kernel": (ctypes.c_int, [_P, ctypes.c_int,
+                                                   ctypes.POINTER(ctypes.c_double),
+                                                   ctypes.POINTER(ctypes.c_double)]),
+    "fqlpop_flops_per_member_step": (ctypes.c_double, [ctypes.POINTER(Config)]),
+}
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load libfqlpop.so (no fallback: raises if it is missing)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise FqlpopError(
+            f"{p} not found: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load_library().fqlpop_last_error().decode(errors="replace")
+        raise FqlpopError(f"fqlpop error {rc}: {msg}")
+
+
+def fptr(a):
+    """float32 C-contiguous numpy array -> float* (the array must stay alive)."""
+    return a.ctypes.data_as(_F)

@@ -1,0 +1,174 @@
+/*
+ * fqlpop.h -- C ABI of the MI355X-native FQL population trainer (libfqlpop.so).
+ *
+ * The reference's boundary for this path is a Python object API, not an FFI
+ * (SURVEY.md section 8b): the callers use FQLAgent.create / update /
+ * total_loss / sample_actions / config and flax (to|from)_state_dict of the
+ * un-vendored `fql` submodule [EXT].  Each entry point below cites the
+ * reference call site it replaces.  The Python shim
+ * `flow-q-learning_amd/fql/agents/fql.py` binds these with ctypes (see
+ * INTEGRATION.md); nothing here uses torch or C++ types.
+ *
+ * Conventions
+ *   - every function returns 0 on success or a negative FQLPOP_E* code; the
+ *     message of the last failure on the calling thread is fqlpop_last_error();
+ *   - the handle owns all device memory (params, Adam moments, target critic,
+ *     dataset copy, activations, info); host pointers are borrowed for the
+ *     duration of the call only;
+ *   - calls are stream-ordered on the handle's streams; functions that return
+ *     data to the host (read_info, get_state, sample_actions) synchronise;
+ *   - one handle per host thread.
+ *   - "member" indices are population slots 0..n_members-1.
+ */
+#ifndef FQLPOP_H
+#define FQLPOP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FQLPOP_OK 0
+#define FQLPOP_E_ARG (-1)      /* bad argument / shape */
+#define FQLPOP_E_HIP (-2)      /* HIP runtime failure */
+#define FQLPOP_E_STATE (-3)    /* call not valid in the current state */
+#define FQLPOP_E_UNSUPPORTED (-4)
+
+/* Number of float slots per member in the info buffers (13 used for train,
+ * 10 for val, in the order of FQLPOP_INFO_*). */
+#define FQLPOP_INFO_STRIDE 16
+enum {
+    FQLPOP_INFO_CRITIC_LOSS = 0, FQLPOP_INFO_Q_MEAN, FQLPOP_INFO_Q_MAX, FQLPOP_INFO_Q_MIN,
+    FQLPOP_INFO_ACTOR_LOSS, FQLPOP_INFO_BC_FLOW_LOSS, FQLPOP_INFO_DISTILL_LOSS,
+    FQLPOP_INFO_Q_LOSS, FQLPOP_INFO_Q, FQLPOP_INFO_MSE,
+    FQLPOP_INFO_GRAD_MAX, FQLPOP_INFO_GRAD_MIN, FQLPOP_INFO_GRAD_NORM
+};
+
+/* Which state buffer get_state/set_state address. */
+enum { FQLPOP_STATE_PARAMS = 0, FQLPOP_STATE_ADAM_M = 1, FQLPOP_STATE_ADAM_V = 2 };
+
+/* Mirrors trainer/config.py:5-22 (AgentConfig) for the fields update() reads. */
+typedef struct fqlpop_config {
+    int obs_dim;           /* ob_dims[-1]; set by FQLAgent.create from ex_observations */
+    int action_dim;        /* set by FQLAgent.create from ex_actions */
+    int hidden_dim;        /* width of every hidden layer (actor_hidden_dims == value_hidden_dims) */
+    int num_hidden;        /* number of hidden layers (4) */
+    int batch_size;        /* AgentConfig.batch_size (256 / 1024) */
+    int num_qs;            /* critic ensemble size (2) */
+    int layer_norm;        /* critic LayerNorm (scripts pass --agent.layer_norm) */
+    int actor_layer_norm;  /* actor LayerNorm (False) */
+    int flow_steps;        /* Euler steps (10) */
+    int q_agg_min;         /* q_agg == "min" (else "mean") */
+    int normalize_q_loss;  /* normalize_q_loss */
+    float discount;        /* 0.99 */
+    float tau;             /* 0.005 */
+    float lr;              /* Adam learning rate 3e-4 */
+    int use_graph;         /* capture each step into a hipGraph (1) or launch eagerly (0) */
+} fqlpop_config;
+
+typedef struct fqlpop fqlpop_t;
+
+/* Message of the last failed call on this thread ("" if none). */
+const char* fqlpop_last_error(void);
+
+/* Replaces FQLAgent.create(seed, ex_obs, ex_act, config)  [EXT]
+ * (called at trainer/experiment.py:44-49, utils/agent.py:24-29) for a whole
+ * population: allocates the device state for n_members members, member i
+ * with alpha alphas[i] and seed seeds[i]; params are initialised on device
+ * (Glorot-uniform kernels, zero biases, unit LN scale, target := critic). */
+int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas,
+                  const uint64_t* seeds, int device, fqlpop_t** out);
+
+/* Frees every device allocation of the handle. */
+int fqlpop_destroy(fqlpop_t* h);
+
+/* Replaces the ReplayBuffer/Dataset behind OfflineTaskWithRealEvaluations
+ * (task/offline_task_real.py:26-36; sampled at :38-43).  which = 0 train,
+ * 1 val.  Row-major host arrays obs[n][obs_dim], act[n][action_dim], rew[n],
+ * mask[n], next_obs[n][obs_dim]; copied into an HBM-resident buffer.  If
+ * on_device != 0 the pointers are device pointers on the handle's device. */
+int fqlpop_set_dataset(fqlpop_t* h, int which, const float* obs, const float* act,
+                       const float* rew, const float* mask, const float* next_obs,
+                       int64_t n_rows, int on_device);
+
+/* Selects the members that step()/total_loss() advance (SuccessiveHalving
+ * pruning, hpo/successive_halving.py:67-101; Experiment.stop at
+ * trainer/trainer.py:114-116).  mask[n_members], nonzero = active. */
+int fqlpop_set_active(fqlpop_t* h, const uint8_t* mask);
+
+/* Replaces n_steps iterations of the Experiment.train hot loop
+ * (trainer/experiment.py:106-109): for every active member, sample a
+ * minibatch on device (uniform with replacement, Philox keyed by the member
+ * seed and update count) and run agent.update(batch) [EXT FQLAgent.update]. */
+int fqlpop_step(fqlpop_t* h, int n_steps);
+
+/* Parity mode of agent.update(batch): one update of every active member on
+ * injected data.  batch: per active member (in slot order) the row-major
+ * block [obs B*D][act B*A][rew B][mask B][next_obs B*D]; noise: per active
+ * member [z_next B*A][x0 B*A][t B][z_d B*A][z_metric B*A].  Host pointers. */
+int fqlpop_step_injected(fqlpop_t* h, const float* batch, const float* noise);
+
+/* Replaces agent.total_loss(val_batch, grad_params=None)
+ * (trainer/experiment.py:114-115): losses of every active member, no update.
+ * batch/noise NULL => sample from the val dataset (which = 1, or the train
+ * dataset if no val dataset was set) with device RNG; else injected as in
+ * fqlpop_step_injected. Results via fqlpop_read_info(h, 1, ...). */
+int fqlpop_total_loss(fqlpop_t* h, const float* batch, const float* noise);
+
+/* Copies info[n_members][FQLPOP_INFO_STRIDE] of the last train step (which=0)
+ * or last total_loss (which=1) to the host; synchronises.  Replaces the
+ * update_info / val_info dicts (trainer/experiment.py:109,115). */
+int fqlpop_read_info(fqlpop_t* h, int which, float* out);
+
+/* Replaces agent.sample_actions(observations=obs, seed=..)
+ * (evaluator/evaluation.py:58-64,94): clip(onestep(s, z), -1, 1) for n rows of
+ * member `member`.  noise[n][action_dim] (host) or NULL => z ~ N(0,1) from
+ * Philox(seed).  obs[n][obs_dim], out[n][action_dim] host arrays. */
+int fqlpop_sample_actions(fqlpop_t* h, int member, const float* obs, int64_t n,
+                          const float* noise, uint64_t seed, float* out);
+
+/* Number of floats of one member's flat state (flax tree order: networks
+ * actor_bc_flow, actor_onestep_flow, critic, target_critic; leaves sorted as
+ * flax does).  which = FQLPOP_STATE_*; M/V have the same layout as PARAMS
+ * (target leaves are zero in M/V). */
+int fqlpop_state_size(fqlpop_t* h, int64_t* n_floats);
+
+/* flax.serialization.to_state_dict / from_state_dict of one member
+ * (trainer/experiment.py:61-63,92,135; utils/agent.py:35): copy the flat
+ * state out of / into device memory; synchronises. */
+int fqlpop_get_state(fqlpop_t* h, int member, int which, float* flat, int64_t n);
+int fqlpop_set_state(fqlpop_t* h, int member, int which, const float* flat, int64_t n);
+
+/* Adam step count of a member (optax count == number of updates). */
+int fqlpop_get_count(fqlpop_t* h, int member, int32_t* count);
+int fqlpop_set_count(fqlpop_t* h, int member, int32_t count);
+
+/* Per-member alpha and seed (ExperimentConfig.alpha/seed,
+ * trainer/config.py:25-28); re-initialises params when reinit != 0. */
+int fqlpop_set_member(fqlpop_t* h, int member, float alpha, uint64_t seed, int reinit);
+
+/* Leaf table of the flat state: name (e.g. "critic/Dense_0/kernel"), offset
+ * and shape (up to 3 dims, ndim returned).  i in [0, fqlpop_num_leaves). */
+int fqlpop_num_leaves(fqlpop_t* h, int* n);
+int fqlpop_leaf_info(fqlpop_t* h, int i, char* name, int name_cap, int64_t* offset,
+                     int* ndim, int64_t* shape3);
+
+/* Waits for all work of the handle. */
+int fqlpop_sync(fqlpop_t* h);
+
+/* Measurement hook for bench.py: replays the dominant kernel (the hidden-
+ * layer forward GEMM of the Euler flow, all active members in one launch)
+ * `iters` times on its own stream between HIP events; returns the mean
+ * duration (us) and the algorithmic FLOPs of one launch. */
+int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* flops);
+
+/* Algorithmic GEMM FLOPs of one member-update at the handle's config
+ * (SURVEY.md 8d formula). */
+double fqlpop_flops_per_member_step(const fqlpop_config* cfg);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FQLPOP_H */
