@@ -100,23 +100,31 @@ DEV int xcd_remap(int bid, int total) {
 // consecutive floats: conflict-free ds_read_b32); r-contiguous operands are
 // stored [i][r] with row pitch BK+1 (bank = (i + r) mod 32: conflict-free).
 
+// Buffer resources: a raw buffer load past `num_records` bytes returns 0, so
+// the K tail of the first layer (K = 33/34) and the 33/34-row dW of the
+// first layer need no per-element guard (a guarded load compiles to a
+// branch + s_waitcnt vmcnt(0) per load, which serialises the pipeline).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+DEV rsrc_t make_rsrc(const float* p, long long n_elems) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(n_elems * 4), 0x00020000);
+}
+DEV float4 bload4(rsrc_t r, int elem_off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, elem_off * 4, 0, 0));
+}
+
 // Global -> register staging of one operand slice.  An "IC" (i-contiguous)
 // operand slice is BK rows (r) x TILE cols (i); an "RC" slice is TILE rows (i)
-// x BK cols (r).  Element p of the thread's float4 list; rows beyond `rows`
-// or columns beyond `cols` read as zero.
+// x BK cols (r).  Element p of the thread's float4 list.
 template <int TILE, int BK, bool RC>
-DEV float4 stage_load(const float* __restrict__ X, int ld, int p, int i0, int k0, int ilim, int klim) {
+DEV float4 stage_load(rsrc_t X, int ld, int p, int i0, int k0) {
     const int idx = threadIdx.x + 256 * p;
     if constexpr (RC) {
         const int row = idx / (BK / 4), c = (idx % (BK / 4)) * 4;
-        const int gi = i0 + row, gr = k0 + c;
-        if (gi < ilim && gr < klim) return *reinterpret_cast<const float4*>(X + (long long)gi * ld + gr);
+        return bload4(X, (i0 + row) * ld + k0 + c);
     } else {
         const int row = idx / (TILE / 4), c = (idx % (TILE / 4)) * 4;
-        const int gr = k0 + row, gi = i0 + c;
-        if (gr < klim && gi < ilim) return *reinterpret_cast<const float4*>(X + (long long)gr * ld + gi);
+        return bload4(X, (k0 + row) * ld + i0 + c);
     }
-    return make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 template <int TILE, int BK, bool RC>
@@ -140,9 +148,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
     constexpr int B_SZ = BRC ? BN * (BK + 1) : BK * BN;
     constexpr int A_LD = BM * BK / 1024;  // float4 loads per thread
     constexpr int B_LD = BN * BK / 1024;
-    __shared__ __attribute__((aligned(16))) float smem[2 * (A_SZ + B_SZ)];
+    __shared__ __attribute__((aligned(16))) float smem[2 * (A_SZ + B_SZ) + BM];
 
-    const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
+    const int tiles_m = g.M / BM + (g.M % BM != 0), tiles_n = g.N / BN;  // host guarantees N % BN == 0
     const int per = tiles_m * tiles_n;
     const int total = per * g.ny * g.nz;
     const int w = xcd_remap(blockIdx.x, total);
@@ -150,15 +158,25 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
     const int y = yz % g.ny, z = yz / g.ny;
     const int slot = g.slots[z];
     const int i0 = (tile / tiles_n) * BM, j0 = (tile % tiles_n) * BN;
-
-    const float* __restrict__ A = at(g.A, slot, y);
-    const float* __restrict__ B = at(g.B, slot, y);
-    const int tid = threadIdx.x;
-    // scalar copies: lambdas must not capture the kernarg struct by reference
-    // (that materialises it in scratch)
     const int gM = g.M, gN = g.N, gK = g.K, lda = g.lda, ldb = g.ldb;
 
-    float4 ra[A_LD], rb[B_LD];
+    // valid extents (elements) of the two operands from their base
+    const rsrc_t rA = make_rsrc(at(g.A, slot, y), ARC ? (long long)(gM - 1) * lda + gK : (long long)(gK - 1) * lda + gM);
+    const rsrc_t rB = make_rsrc(at(g.B, slot, y), BRC ? (long long)(gN - 1) * ldb + gK : (long long)(gK - 1) * ldb + gN);
+
+    float* As0 = smem;
+    float* Bs0 = smem + A_SZ;
+    float* As1 = smem + A_SZ + B_SZ;
+    float* Bs1 = As1 + A_SZ;
+    float* bias_s = smem + 2 * (A_SZ + B_SZ);
+    if constexpr (EPI != EPI_STORE) {
+        if (threadIdx.x < BM) {
+            const int i = i0 + threadIdx.x;
+            bias_s[threadIdx.x] = i < gM ? at(g.bias, slot, y)[i] : 0.f;
+        }
+    }
+
+    const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wi = (wave >> 1) * WM, wj = (wave & 1) * WN;
     const int l32 = lane & 31, lh = lane >> 5;
@@ -171,89 +189,101 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-    float* As0 = smem;
-    float* Bs0 = smem + A_SZ;
-    float* As1 = smem + A_SZ + B_SZ;
-    float* Bs1 = As1 + A_SZ;
-
+    float4 ra[A_LD], rb[B_LD];
     const int nk = (gK + BK - 1) / BK;
-#define FQ_LOAD(k0)                                                                              \
-    _Pragma("unroll") for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, ARC>(A, lda, p, i0, k0, gM, gK); \
-    _Pragma("unroll") for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, BRC>(B, ldb, p, j0, k0, gN, gK);
-#define FQ_STORE(As, Bs)                                                                         \
-    _Pragma("unroll") for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, ARC>(As, p, ra[p]);     \
-    _Pragma("unroll") for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC>(Bs, p, rb[p]);
-    FQ_LOAD(0)
-    FQ_STORE(As0, Bs0)
+#pragma unroll
+    for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, ARC>(rA, lda, p, i0, 0);
+#pragma unroll
+    for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, BRC>(rB, ldb, p, j0, 0);
+#pragma unroll
+    for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, ARC>(As0, p, ra[p]);
+#pragma unroll
+    for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC>(Bs0, p, rb[p]);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const float* Ac = (kt & 1) ? As1 : As0;
         const float* Bc = (kt & 1) ? Bs1 : Bs0;
-        const bool more = kt + 1 < nk;
-        if (more) {
-            FQ_LOAD((kt + 1) * BK)
-        }
+        // prefetch the next slice (the last iteration re-reads a valid slice:
+        // no branch, so the loads stay in flight across the MFMAs)
+        const int kn = (kt + 1 < nk ? kt + 1 : kt) * BK;
+#pragma unroll
+        for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, ARC>(rA, lda, p, i0, kn);
+#pragma unroll
+        for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, BRC>(rB, ldb, p, j0, kn);
+        // keep the prefetch at the top of the iteration (hipcc otherwise sinks
+        // it next to its ds_write and exposes the whole global latency)
+        __builtin_amdgcn_sched_barrier(0);
+        // all fragments of the slice first, then the MFMA chain
+        float av[BK / 2][TM], bv[BK / 2][TN];
 #pragma unroll
         for (int kk = 0; kk < BK / 2; ++kk) {
             const int rr = 2 * kk + lh;
-            float av[TM], bv[TN];
 #pragma unroll
             for (int a = 0; a < TM; ++a)
-                av[a] = ARC ? Ac[(wi + a * 32 + l32) * (BK + 1) + rr] : Ac[rr * BM + wi + a * 32 + l32];
+                av[kk][a] = ARC ? Ac[(wi + a * 32 + l32) * (BK + 1) + rr] : Ac[rr * BM + wi + a * 32 + l32];
 #pragma unroll
             for (int b = 0; b < TN; ++b)
-                bv[b] = BRC ? Bc[(wj + b * 32 + l32) * (BK + 1) + rr] : Bc[rr * BN + wj + b * 32 + l32];
+                bv[kk][b] = BRC ? Bc[(wj + b * 32 + l32) * (BK + 1) + rr] : Bc[rr * BN + wj + b * 32 + l32];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; ++kk)
 #pragma unroll
             for (int a = 0; a < TM; ++a)
 #pragma unroll
                 for (int b = 0; b < TN; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
-        }
-        if (more) {
-            float* An = (kt & 1) ? As0 : As1;
-            float* Bn = (kt & 1) ? Bs0 : Bs1;
-            FQ_STORE(An, Bn)
-        }
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk][a], bv[kk][b], acc[a][b], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        float* An = (kt & 1) ? As0 : As1;
+        float* Bn = (kt & 1) ? Bs0 : Bs1;
+#pragma unroll
+        for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, ARC>(An, p, ra[p]);
+#pragma unroll
+        for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC>(Bn, p, rb[p]);
         __syncthreads();
     }
-#undef FQ_LOAD
-#undef FQ_STORE
 
     // epilogue: accumulator register r of a 32x32 tile holds
     // row i = (r&3) + 8*(r>>2) + 4*(lane>>5), column j = lane&31.
     float* __restrict__ C = at(g.C, slot, y);
     float* __restrict__ C2 = (EPI == EPI_BIAS_GELU2) ? at(g.C2, slot, y) : nullptr;
-    const float* __restrict__ bias = (EPI != EPI_STORE) ? at(g.bias, slot, y) : nullptr;
+    const int ldc = g.ldc;
+    const bool full = i0 + BM <= gM;  // uniform: no row guard needed
 #pragma unroll
-    for (int a = 0; a < TM; ++a)
+    for (int a = 0; a < TM; ++a) {
+        float bsv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            bsv[r] = (EPI != EPI_STORE) ? bias_s[wi + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh] : 0.f;
 #pragma unroll
         for (int b = 0; b < TN; ++b)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int i = i0 + wi + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
                 const int j = j0 + wj + b * 32 + l32;
-                if (i < g.M && j < g.N) {
+                if (full || i < gM) {
                     float v = acc[a][b][r];
-                    const long long o = (long long)i * g.ldc + j;
+                    const long long o = (long long)i * ldc + j;
                     if constexpr (EPI == EPI_STORE) {
                         C[o] = v;
                     } else if constexpr (EPI == EPI_BIAS) {
-                        C[o] = v + bias[i];
+                        C[o] = v + bsv[r];
                     } else if constexpr (EPI == EPI_BIAS_GELU2) {
-                        v += bias[i];
+                        v += bsv[r];
                         C[o] = v;
                         C2[o] = gelu_f(v);
                     } else {
-                        C[o] = gelu_f(v + bias[i]);
+                        C[o] = gelu_f(v + bsv[r]);
                     }
                 }
             }
+    }
 }
 
 template <bool ARC, bool BRC, int EPI>
 static void gemm_dispatch_tile(int tile, const GemmArgs& a, hipStream_t s) {
     auto grid = [&](int bm, int bn) {
-        return dim3(((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) * a.ny * a.nz);
+        return dim3(((a.M + bm - 1) / bm) * (a.N / bn) * a.ny * a.nz);
     };
     switch (tile) {
         case 0: hipLaunchKernelGGL((gemm_kernel<64, 64, ARC, BRC, EPI>), grid(64, 64), dim3(256), 0, s, a); break;
@@ -264,6 +294,13 @@ static void gemm_dispatch_tile(int tile, const GemmArgs& a, hipStream_t s) {
 }
 
 void launch_gemm(int layout, int epi, int tile, const GemmArgs& a, hipStream_t s) {
+    // column tiles must divide N exactly (no column guard in the kernel)
+    if ((tile & 2) && a.N % 128 != 0) tile &= ~2;
+    if (layout != LAYOUT_FWD && a.K % 32 != 0) {
+        // r-contiguous operands are read in whole 32-wide slices
+        (void)hipErrorInvalidValue;
+        return;
+    }
     if (layout == LAYOUT_FWD) {
         switch (epi) {
             case EPI_BIAS: gemm_dispatch_tile<false, false, EPI_BIAS>(tile, a, s); break;
@@ -277,56 +314,85 @@ void launch_gemm(int layout, int epi, int tile, const GemmArgs& a, hipStream_t s
     }
 }
 
+// ================================================= column-reduction kernels ==
+// Kernels that reduce over the FEATURE axis for every column (minibatch row)
+// m: LayerNorm statistics, the narrow last Dense layer, the LN backward row
+// statistics and the critic input gradient.  A block owns 64 columns (one per
+// lane, coalesced 256 B rows) and 16 waves split the H features, KPT = H/16
+// each; every thread issues its KPT loads before consuming any of them (the
+// latency of one HBM round trip per block instead of KPT of them) and the 16
+// partial results meet in LDS.
+constexpr int CW = 16;  // waves per column block
+
+#define FQ_KPT_DISPATCH(H, KERNEL, ...)                                      \
+    switch ((H) / CW) {                                                      \
+        case 4: KERNEL(4, __VA_ARGS__); break;                               \
+        case 8: KERNEL(8, __VA_ARGS__); break;                               \
+        case 16: KERNEL(16, __VA_ARGS__); break;                             \
+        case 32: KERNEL(32, __VA_ARGS__); break;                             \
+        default: KERNEL(64, __VA_ARGS__); break;                             \
+    }
+
 // ======================================================= LayerNorm fwd =====
 // h'[k][m] = (gelu(u'[k][m]) - mu[m]) * rstd[m] * gamma[k] + beta[k]
-// (flax LayerNorm eps 1e-6, fast variance, after GELU).  Block = 64 columns x
-// 4 waves splitting the features; stats combined through LDS.
-__global__ __launch_bounds__(256) void ln_gelu_fwd_kernel(const LnArgs a) {
+// (flax LayerNorm eps 1e-6, fast variance E[g^2]-E[g]^2 clipped at 0, applied
+// after GELU).  gelu(u) stays in registers between the statistics and the
+// normalisation.
+template <int KPT>
+__global__ __launch_bounds__(1024) void ln_gelu_fwd_kernel(const LnArgs a) {
     const int ncb = a.M / 64;
     const int cb = blockIdx.x % ncb, yz = blockIdx.x / ncb;
     const int y = yz % a.ny, z = yz / a.ny;
     const int slot = a.slots[z];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int m = cb * 64 + lane;
-    const float* __restrict__ u = at(a.u, slot, y);
-    float* __restrict__ h = at(a.h, slot, y);
-    const float* __restrict__ gam = at(a.gamma, slot, y);
-    const float* __restrict__ bet = at(a.beta, slot, y);
-    const int kq = a.H / 4, k0 = w * kq;
+    const long long ld = a.ld;
+    const float* __restrict__ u = at(a.u, slot, y) + m;
+    const int k0 = w * KPT;
+    float g[KPT];
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) g[i] = u[(k0 + i) * ld];
     float s1 = 0.f, s2 = 0.f;
-    for (int k = k0; k < k0 + kq; ++k) {
-        const float gv = gelu_f(u[(long long)k * a.ld + m]);
-        s1 += gv;
-        s2 += gv * gv;
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+        g[i] = gelu_f(g[i]);
+        s1 += g[i];
+        s2 += g[i] * g[i];
     }
-    __shared__ float red[2][4][64];
+    __shared__ float red[2][CW][64];
     red[0][w][lane] = s1;
     red[1][w][lane] = s2;
     __syncthreads();
-    const float S1 = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
-    const float S2 = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+    float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < CW; ++q) {
+        S1 += red[0][q][lane];
+        S2 += red[1][q][lane];
+    }
     const float mean = S1 / (float)a.H;
     const float var = fmaxf(S2 / (float)a.H - mean * mean, 0.f);
     const float rs = 1.0f / sqrtf(var + 1e-6f);
-    for (int k = k0; k < k0 + kq; ++k) {
-        const long long o = (long long)k * a.ld + m;
-        const float gv = gelu_f(u[o]);
-        h[o] = (gv - mean) * rs * gam[k] + bet[k];
-    }
+    float* __restrict__ h = at(a.h, slot, y) + m;
+    const float* __restrict__ gam = at(a.gamma, slot, y) + k0;
+    const float* __restrict__ bet = at(a.beta, slot, y) + k0;
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) h[(k0 + i) * ld] = (g[i] - mean) * rs * gam[i] + bet[i];
     if (w == 0) {
         at(a.mu, slot, y)[m] = mean;
         at(a.rstd, slot, y)[m] = rs;
     }
 }
 
+#define FQ_LN_LAUNCH(KPT, grid, s, a) hipLaunchKernelGGL(ln_gelu_fwd_kernel<KPT>, grid, dim3(1024), 0, s, a)
 void launch_ln_gelu_fwd(const LnArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(ln_gelu_fwd_kernel, dim3((a.M / 64) * a.ny * a.nz), dim3(256), 0, s, a);
+    const dim3 grid((a.M / 64) * a.ny * a.nz);
+    FQ_KPT_DISPATCH(a.H, FQ_LN_LAUNCH, grid, s, a)
 }
 
 // ============================================================ head fwd =====
-// Last Dense layer (out width 1 or action_dim <= 8): one lane per column,
-// weights are wave-uniform (scalar loads); 4 waves split the features.
-// Modes fuse what consumes the head output:
+// Last Dense layer (out width 1 or action_dim <= 8): weights are wave-uniform
+// (scalar loads).  Modes fuse what consumes the head output:
 //   HEAD_STORE    o0[j][m] = v                              (critic Q)
 //   HEAD_BC_FUSED M = 2B: m <  B -> o0 = v_theta prediction (BC loss)
 //                         m >= B -> Euler step 0: x1 = z_d + v/steps into o2
@@ -337,7 +403,47 @@ void launch_ln_gelu_fwd(const LnArgs& a, hipStream_t s) {
 //                 [2B,3B) clip(v) -> o3 (mse metric actions)
 //   HEAD_ACT      o0 = clip(v)                              (sample_actions)
 template <int MODE>
-__global__ __launch_bounds__(256) void head_fwd_kernel(const HeadArgs a) {
+DEV void head_write(const HeadArgs& a, int slot, int y, int j, int m, float v) {
+    const int B = a.B, D = a.D;
+    if constexpr (MODE == HEAD_STORE) {
+        at(a.o0, slot, y)[(long long)j * a.ld0 + m] = v;
+    } else if constexpr (MODE == HEAD_ACT) {
+        at(a.o0, slot, y)[(long long)j * a.ld0 + m] = clip1(v);
+    } else if constexpr (MODE == HEAD_BC_FUSED) {
+        if (m < B) {
+            at(a.o0, slot)[(long long)j * a.ld0 + m] = v;
+        } else {
+            const int mm = m - B;
+            const float x = at(a.o1, slot)[(long long)(D + j) * a.ld1 + m];
+            float* eu = at(a.o2, slot);
+            eu[(long long)(D + j) * a.ld2 + mm] = x + v / a.steps_f;
+            if (j == 0) eu[(long long)(D + a.nout) * a.ld2 + mm] = a.t_next;
+        }
+    } else if constexpr (MODE == HEAD_EULER) {
+        float* eu = at(a.o2, slot);
+        const long long o = (long long)(D + j) * a.ld2 + m;
+        const float xn = eu[o] + v / a.steps_f;
+        if (a.last) {
+            at(a.o0, slot)[(long long)j * a.ld0 + m] = clip1(xn);
+        } else {
+            eu[o] = xn;
+            if (j == 0) eu[(long long)(D + a.nout) * a.ld2 + m] = a.t_next;
+        }
+    } else if constexpr (MODE == HEAD_OS) {
+        if (m < B) {
+            at(a.o1, slot)[(long long)(D + j) * a.ld1 + m] = clip1(v);
+        } else if (m < 2 * B) {
+            const int mm = m - B;
+            at(a.o0, slot)[(long long)j * a.ld0 + mm] = v;
+            at(a.o2, slot)[(long long)(D + j) * a.ld2 + B + mm] = clip1(v);
+        } else {
+            at(a.o3, slot)[(long long)j * a.ld3 + (m - 2 * B)] = clip1(v);
+        }
+    }
+}
+
+template <int MODE, int KPT>
+__global__ __launch_bounds__(1024) void head_fwd_kernel(const HeadArgs a) {
     const int ncb = a.M / 64;
     const int cb = blockIdx.x % ncb, yz = blockIdx.x / ncb;
     const int y = yz % a.ny, z = yz / a.ny;
@@ -345,75 +451,47 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const HeadArgs a) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int m = cb * 64 + lane;
-    const float* __restrict__ h = at(a.h, slot, y);
-    const float* __restrict__ W = at(a.W, slot, y);
+    const long long ld = a.ld;
     const int nout = a.nout;
+    const int k0 = w * KPT;
+    const float* __restrict__ h = at(a.h, slot, y) + m;
+    const float* __restrict__ W = at(a.W, slot, y) + (long long)k0 * nout;
+    float hv[KPT];
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) hv[i] = h[(k0 + i) * ld];
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    const int kq = a.H / 4, k0 = w * kq;
-    for (int k = k0; k < k0 + kq; ++k) {
-        const float hv = h[(long long)k * a.ld + m];
-        const float* wr = W + (long long)k * nout;
+#pragma unroll
+    for (int i = 0; i < KPT; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-            if (j < nout) acc[j] += wr[j] * hv;
-    }
-    __shared__ float red[4][8][64];
+            if (j < nout) acc[j] += W[i * nout + j] * hv[i];
+    __shared__ float red[CW][8][64];
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[w][j][lane] = acc[j];
     __syncthreads();
-    if (w != 0) return;
-    const float* __restrict__ bias = at(a.b, slot, y);
-    const int B = a.B, D = a.D;
-    for (int j = 0; j < nout; ++j) {
-        const float v = (red[0][j][lane] + red[1][j][lane]) + (red[2][j][lane] + red[3][j][lane]) + bias[j];
-        if constexpr (MODE == HEAD_STORE) {
-            at(a.o0, slot, y)[(long long)j * a.ld0 + m] = v;
-        } else if constexpr (MODE == HEAD_ACT) {
-            at(a.o0, slot, y)[(long long)j * a.ld0 + m] = clip1(v);
-        } else if constexpr (MODE == HEAD_BC_FUSED) {
-            if (m < B) {
-                at(a.o0, slot)[(long long)j * a.ld0 + m] = v;
-            } else {
-                const int mm = m - B;
-                const float x = at(a.o1, slot)[(long long)(D + j) * a.ld1 + m];
-                float* eu = at(a.o2, slot);
-                eu[(long long)(D + j) * a.ld2 + mm] = x + v / a.steps_f;
-                if (j == 0) eu[(long long)(D + nout) * a.ld2 + mm] = a.t_next;
-            }
-        } else if constexpr (MODE == HEAD_EULER) {
-            float* eu = at(a.o2, slot);
-            const long long o = (long long)(D + j) * a.ld2 + m;
-            const float xn = eu[o] + v / a.steps_f;
-            if (a.last) {
-                at(a.o0, slot)[(long long)j * a.ld0 + m] = clip1(xn);
-            } else {
-                eu[o] = xn;
-                if (j == 0) eu[(long long)(D + nout) * a.ld2 + m] = a.t_next;
-            }
-        } else if constexpr (MODE == HEAD_OS) {
-            if (m < B) {
-                at(a.o1, slot)[(long long)(D + j) * a.ld1 + m] = clip1(v);
-            } else if (m < 2 * B) {
-                const int mm = m - B;
-                at(a.o0, slot)[(long long)j * a.ld0 + mm] = v;
-                at(a.o2, slot)[(long long)(D + j) * a.ld2 + B + mm] = clip1(v);
-            } else {
-                at(a.o3, slot)[(long long)j * a.ld3 + (m - 2 * B)] = clip1(v);
-            }
-        }
+    const int t = threadIdx.x;
+    if (t < nout * 64) {
+        const int j = t >> 6, l2 = t & 63;
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < CW; ++q) v += red[q][j][l2];
+        v += at(a.b, slot, y)[j];
+        head_write<MODE>(a, slot, y, j, cb * 64 + l2, v);
     }
 }
 
+#define FQ_HEAD_LAUNCH(KPT, MODE, grid, s, a) \
+    hipLaunchKernelGGL((head_fwd_kernel<MODE, KPT>), grid, dim3(1024), 0, s, a)
 void launch_head_fwd(int mode, const HeadArgs& a, hipStream_t s) {
-    const dim3 grid((a.M / 64) * a.ny * a.nz), blk(256);
+    const dim3 grid((a.M / 64) * a.ny * a.nz);
     switch (mode) {
-        case HEAD_STORE: hipLaunchKernelGGL(head_fwd_kernel<HEAD_STORE>, grid, blk, 0, s, a); break;
-        case HEAD_BC_FUSED: hipLaunchKernelGGL(head_fwd_kernel<HEAD_BC_FUSED>, grid, blk, 0, s, a); break;
-        case HEAD_EULER: hipLaunchKernelGGL(head_fwd_kernel<HEAD_EULER>, grid, blk, 0, s, a); break;
-        case HEAD_OS: hipLaunchKernelGGL(head_fwd_kernel<HEAD_OS>, grid, blk, 0, s, a); break;
-        default: hipLaunchKernelGGL(head_fwd_kernel<HEAD_ACT>, grid, blk, 0, s, a); break;
+        case HEAD_STORE: FQ_KPT_DISPATCH(a.H, FQ_HEAD_LAUNCH, HEAD_STORE, grid, s, a) break;
+        case HEAD_BC_FUSED: FQ_KPT_DISPATCH(a.H, FQ_HEAD_LAUNCH, HEAD_BC_FUSED, grid, s, a) break;
+        case HEAD_EULER: FQ_KPT_DISPATCH(a.H, FQ_HEAD_LAUNCH, HEAD_EULER, grid, s, a) break;
+        case HEAD_OS: FQ_KPT_DISPATCH(a.H, FQ_HEAD_LAUNCH, HEAD_OS, grid, s, a) break;
+        default: FQ_KPT_DISPATCH(a.H, FQ_HEAD_LAUNCH, HEAD_ACT, grid, s, a) break;
     }
 }
 
@@ -437,8 +515,8 @@ DEV float load_dh(const float* __restrict__ dh, const float* __restrict__ W5, co
 
 // LN backward row statistics: c1[m] = mean_k(dxhat), c2[m] = mean_k(dxhat*xhat)
 // with dxhat = dh*gamma, xhat = (gelu(u)-mu)*rstd.
-template <bool HEAD>
-__global__ __launch_bounds__(256) void bwd_rowstats_kernel(const BwdArgs a) {
+template <bool HEAD, int KPT>
+__global__ __launch_bounds__(1024) void bwd_rowstats_kernel(const BwdArgs a) {
     const int ncb = a.M / 64;
     const int cb = blockIdx.x % ncb, yz = blockIdx.x / ncb;
     const int y = yz % a.ny, z = yz / a.ny;
@@ -446,33 +524,60 @@ __global__ __launch_bounds__(256) void bwd_rowstats_kernel(const BwdArgs a) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int m = cb * 64 + lane;
-    const float* __restrict__ u = at(a.u, slot, y);
-    const float* __restrict__ dh = HEAD ? nullptr : at(a.dh, slot, y);
-    const float* __restrict__ W5 = HEAD ? at(a.W5, slot, y) : nullptr;
-    const float* __restrict__ gam = at(a.gamma, slot, y);
+    const int k0 = w * KPT;
+    const float* __restrict__ u = at(a.u, slot, y) + m;
+    const float* __restrict__ gam = at(a.gamma, slot, y) + k0;
     const float mu = at(a.mu, slot, y)[m], rs = at(a.rstd, slot, y)[m];
     float dov[8];
+    const float* W5 = nullptr;
+    const float* dh = nullptr;
     if constexpr (HEAD) {
-        const float* dout = at(a.dout, slot, y);
+        const float* dout = at(a.dout, slot, y) + m;
+        W5 = at(a.W5, slot, y) + (long long)k0 * a.nout;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dov[j] = (j < a.nout) ? dout[(long long)j * a.ld_o + m] : 0.f;
+        for (int j = 0; j < 8; ++j) dov[j] = (j < a.nout) ? dout[(long long)j * a.ld_o] : 0.f;
+    } else {
+        dh = at(a.dh, slot, y) + m;
     }
-    const int kq = a.H / 4, k0 = w * kq;
     float s1 = 0.f, s2 = 0.f;
-    for (int k = k0; k < k0 + kq; ++k) {
-        const float dhv = load_dh<HEAD>(dh, W5, dov, a.nout, k, m, a.ld_d);
-        const float xh = (gelu_f(u[(long long)k * a.ld + m]) - mu) * rs;
-        const float dxh = dhv * gam[k];
-        s1 += dxh;
-        s2 += dxh * xh;
+    constexpr int CH = KPT < 16 ? KPT : 16;  // loads in flight per array
+#pragma unroll 1
+    for (int c = 0; c < KPT; c += CH) {
+        float uv[CH], dhv[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) uv[i] = u[(long long)(k0 + c + i) * a.ld];
+        if constexpr (HEAD) {
+#pragma unroll
+            for (int i = 0; i < CH; ++i) {
+                float sv = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j < a.nout) sv += W5[(c + i) * a.nout + j] * dov[j];
+                dhv[i] = sv;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < CH; ++i) dhv[i] = dh[(long long)(k0 + c + i) * a.ld_d];
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const float xh = (gelu_f(uv[i]) - mu) * rs;
+            const float dxh = dhv[i] * gam[c + i];
+            s1 += dxh;
+            s2 += dxh * xh;
+        }
     }
-    __shared__ float red[2][4][64];
+    __shared__ float red[2][CW][64];
     red[0][w][lane] = s1;
     red[1][w][lane] = s2;
     __syncthreads();
     if (w == 0) {
-        const float S1 = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
-        const float S2 = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+        float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < CW; ++q) {
+            S1 += red[0][q][lane];
+            S2 += red[1][q][lane];
+        }
         at(a.c1, slot, y)[m] = S1 / (float)a.H;
         at(a.c2, slot, y)[m] = S2 / (float)a.H;
     }
@@ -557,10 +662,15 @@ __global__ __launch_bounds__(256) void bwd_cols_kernel(const BwdArgs a) {
     }
 }
 
+#define FQ_RS_LAUNCH(KPT, HEAD, grid, s, a) \
+    hipLaunchKernelGGL((bwd_rowstats_kernel<HEAD, KPT>), grid, dim3(1024), 0, s, a)
 void launch_bwd_rowstats(bool head, const BwdArgs& a, hipStream_t s) {
-    const dim3 grid((a.M / 64) * a.ny * a.nz), blk(256);
-    if (head) hipLaunchKernelGGL(bwd_rowstats_kernel<true>, grid, blk, 0, s, a);
-    else hipLaunchKernelGGL(bwd_rowstats_kernel<false>, grid, blk, 0, s, a);
+    const dim3 grid((a.M / 64) * a.ny * a.nz);
+    if (head) {
+        FQ_KPT_DISPATCH(a.H, FQ_RS_LAUNCH, true, grid, s, a)
+    } else {
+        FQ_KPT_DISPATCH(a.H, FQ_RS_LAUNCH, false, grid, s, a)
+    }
 }
 
 void launch_bwd_cols(bool head, bool ln, const BwdArgs& a, hipStream_t s) {
@@ -573,40 +683,49 @@ void launch_bwd_cols(bool head, bool ln, const BwdArgs& a, hipStream_t s) {
 
 // dq/da for the actor's Q term: the critic's first-layer input gradient,
 // restricted to the action rows and summed over the ensemble.
-__global__ __launch_bounds__(256) void input_grad_kernel(const InGradArgs a) {
+template <int KPT>
+__global__ __launch_bounds__(1024) void input_grad_kernel(const InGradArgs a) {
     const int ncb = a.M / 64;
     const int cb = blockIdx.x % ncb, z = blockIdx.x / ncb;
     const int slot = a.slots[z];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int m = cb * 64 + lane;
+    const int n0 = w * KPT;
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    const int nq = a.H / 4, n0 = w * nq;
     for (int e = 0; e < a.E; ++e) {
-        const float* __restrict__ W0 = at(a.W0, slot, e);
-        const float* __restrict__ du = at(a.du0, slot, e);
-        for (int n = n0; n < n0 + nq; ++n) {
-            const float dv = du[(long long)n * a.ld + a.off + m];
+        const float* __restrict__ W0 = at(a.W0, slot, e) + (long long)a.D * a.H + n0;
+        const float* __restrict__ du = at(a.du0, slot, e) + a.off + m;
+        float dv[KPT];
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j < a.A) acc[j] += W0[(long long)(a.D + j) * a.H + n] * dv;
-        }
+        for (int i = 0; i < KPT; ++i) dv[i] = du[(long long)(n0 + i) * a.ld];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j < a.A) {
+#pragma unroll
+                for (int i = 0; i < KPT; ++i) acc[j] += W0[(long long)j * a.H + i] * dv[i];
+            }
     }
-    __shared__ float red[4][8][64];
+    __shared__ float red[CW][8][64];
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[w][j][lane] = acc[j];
     __syncthreads();
-    if (w == 0) {
-        float* da = at(a.da, slot);
-        for (int j = 0; j < a.A; ++j)
-            da[(long long)j * a.M + m] = (red[0][j][lane] + red[1][j][lane]) + (red[2][j][lane] + red[3][j][lane]);
+    const int t = threadIdx.x;
+    if (t < a.A * 64) {
+        const int j = t >> 6, l2 = t & 63;
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < CW; ++q) v += red[q][j][l2];
+        at(a.da, slot)[(long long)j * a.M + cb * 64 + l2] = v;
     }
 }
 
+#define FQ_IG_LAUNCH(KPT, grid, s, a) hipLaunchKernelGGL(input_grad_kernel<KPT>, grid, dim3(1024), 0, s, a)
 void launch_input_grad(const InGradArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(input_grad_kernel, dim3((a.M / 64) * a.nz), dim3(256), 0, s, a);
+    const dim3 grid((a.M / 64) * a.nz);
+    FQ_KPT_DISPATCH(a.H, FQ_IG_LAUNCH, grid, s, a)
 }
 
 // =============================================================== RNG =======

@@ -727,7 +727,11 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         ARGCHK(n_members > 0, "n_members must be > 0");
         ARGCHK(cfg->action_dim >= 1 && cfg->action_dim <= 8, "action_dim must be in [1, 8]");
         ARGCHK(cfg->obs_dim >= 1, "obs_dim must be >= 1");
-        ARGCHK(cfg->hidden_dim >= 64 && cfg->hidden_dim % 64 == 0, "hidden_dim must be a multiple of 64");
+        {
+            const int hd = cfg->hidden_dim;
+            ARGCHK(hd == 64 || hd == 128 || hd == 256 || hd == 512 || hd == 1024,
+                   "hidden_dim must be one of 64, 128, 256, 512, 1024");
+        }
         ARGCHK(cfg->num_hidden >= 1, "num_hidden must be >= 1");
         ARGCHK(cfg->batch_size >= 64 && cfg->batch_size % 64 == 0, "batch_size must be a multiple of 64");
         ARGCHK(cfg->num_qs >= 1 && cfg->num_qs <= 4, "num_qs must be in [1, 4]");
