@@ -123,21 +123,16 @@ def main():
 
     wl = WORKLOADS[args.workload]
     # dataset: generated on rank 0, broadcast over RCCL (xGMI) to every rank
+    from fqlpop import distributed as D
     data = synthetic_dataset(args.rows, wl["obs_dim"], wl["action_dim"]) if rank == 0 else None
-    keys = ("observations", "actions", "rewards", "masks", "next_observations")
     dev = torch.device("cuda", local_rank)
     shapes = {"observations": (args.rows, wl["obs_dim"]), "actions": (args.rows, wl["action_dim"]),
               "rewards": (args.rows,), "masks": (args.rows,), "next_observations": (args.rows, wl["obs_dim"])}
-    dev_data = {}
-    for k in keys:
-        t = torch.from_numpy(data[k]).to(dev) if rank == 0 else torch.empty(shapes[k], dtype=torch.float32, device=dev)
-        if distributed:
-            dist.broadcast(t, src=0)
-        dev_data[k] = t
+    dev_data = D.broadcast_dataset(data, shapes, dev)
     torch.cuda.synchronize()
 
     alphas_all, seeds_all = population_values(args.members * world)
-    alphas, seeds = alphas_all[rank::world], seeds_all[rank::world]
+    alphas, seeds = D.shard(alphas_all, rank, world), D.shard(seeds_all, rank, world)
     pcfg = PopulationConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"], batch_size=wl["batch_size"],
                             use_graph=not args.no_graph)
     pop = Population(pcfg, alphas, seeds, device=local_rank)
@@ -163,9 +158,7 @@ def main():
     el = time.perf_counter() - t0
     if distributed:
         dist.barrier()
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = D.max_over_ranks(el, dev)
     info = pop.read_info_array()
     finite = bool(np.all(np.isfinite(info[:, :13])))
 

@@ -39,6 +39,8 @@ struct GemmArgs {
 };
 // tile: 0 = 64x64, 1 = 128x64 (i x j), 2 = 64x128, 3 = 128x128
 void launch_gemm(int layout, int epi, int tile, const GemmArgs& a, hipStream_t s);
+// variant: bit 0 = K slice 64 (else 32), bit 1 = two accumulator chains
+void launch_gemm_variant(int layout, int epi, int tile, int variant, const GemmArgs& a, hipStream_t s);
 
 // ------------------------------------------------------- row-wise kernels --
 struct LnArgs {           // h = LN(gelu(u)) * gamma + beta, per column

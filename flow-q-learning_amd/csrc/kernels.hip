@@ -140,9 +140,8 @@ DEV void stage_store(float* __restrict__ S, int p, float4 v) {
     }
 }
 
-template <int BM, int BN, bool ARC, bool BRC, int EPI>
+template <int BM, int BN, int BK, bool DUAL, bool ARC, bool BRC, int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
-    constexpr int BK = 32;
     constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
     constexpr int A_SZ = ARC ? BM * (BK + 1) : BK * BM;
     constexpr int B_SZ = BRC ? BN * (BK + 1) : BK * BN;
@@ -181,13 +180,18 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
     const int wi = (wave >> 1) * WM, wj = (wave & 1) * WN;
     const int l32 = lane & 31, lh = lane >> 5;
 
-    f32x16 acc[TM][TN];
+    // DUAL: even / odd k-pairs accumulate into separate registers (two
+    // independent MFMA chains), summed once in the epilogue
+    f32x16 acc[TM][TN], acc2[TM][TN];
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+            for (int r = 0; r < 16; ++r) {
+                acc[a][b][r] = 0.f;
+                acc2[a][b][r] = 0.f;
+            }
 
     float4 ra[A_LD], rb[B_LD];
     const int nk = (gK + BK - 1) / BK;
@@ -232,7 +236,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
             for (int a = 0; a < TM; ++a)
 #pragma unroll
                 for (int b = 0; b < TN; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk][a], bv[kk][b], acc[a][b], 0, 0, 0);
+                    if (DUAL && (kk & 1))
+                        acc2[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk][a], bv[kk][b], acc2[a][b], 0, 0, 0);
+                    else
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk][a], bv[kk][b], acc[a][b], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         float* An = (kt & 1) ? As0 : As1;
         float* Bn = (kt & 1) ? Bs0 : Bs1;
@@ -249,6 +256,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
     float* __restrict__ C2 = (EPI == EPI_BIAS_GELU2) ? at(g.C2, slot, y) : nullptr;
     const int ldc = g.ldc;
     const bool full = i0 + BM <= gM;  // uniform: no row guard needed
+    if constexpr (DUAL) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) acc[a][b] += acc2[a][b];
+    }
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
         float bsv[16];
@@ -280,38 +293,207 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Forward GEMM (both operands i-contiguous: W[k][n] and x'[k][m]) on an
+// LDS-DMA ring.  `buffer_load_dwordx4 ... lds` writes a wave's 64 x 16 B
+// straight into a lane-linear LDS image, so each K slice [BK][TILE] is moved
+// with no VGPR staging and no ds_write; STAGES-1 slices are in flight while
+// one is consumed.  Per iteration: counted vmcnt (own DMAs of slice kt
+// landed) -> raw s_barrier (everyone's landed, everyone done with kt-1) ->
+// DMA slice kt+STAGES-1 into the freed buffer -> fragments -> MFMAs.
+// K tail (first layer, K = 33/34): the buffer range check returns zeros.
+DEV constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | (((n >> 4) & 3) << 14); }
+
+template <int TILE, int BK>
+DEV void dma_slice(rsrc_t r, int ld, int i0, int k0, float* lds_slice, int wave, int lane) {
+    constexpr int NQ = TILE * BK / 256 / 4;  // 1 KB DMA instructions per wave per slice
+#pragma unroll
+    for (int t = 0; t < NQ; ++t) {
+        const int q = wave * NQ + t;  // instruction index within the slice
+        const int f = q * 256 + lane * 4;  // float offset of this lane's 16 B
+        const int row = f / TILE, col = f % TILE;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void*)(lds_slice + q * 256), 16,
+            ((k0 + row) * ld + i0 + col) * 4, 0, 0, 0);
+    }
+}
+
+template <int BM, int BN, int STAGES, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_fwd_dma_kernel(const GemmArgs g) {
+    constexpr int BK = 32;
+    constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+    constexpr int SA = BK * BM, SB = BK * BN, SS = SA + SB;  // floats per stage
+    constexpr int NQ = (SA + SB) / 1024;                       // DMA instructions per wave per stage
+    __shared__ __attribute__((aligned(16))) float smem[STAGES * SS + BM];
+
+    const int tiles_m = g.M / BM, tiles_n = g.N / BN;  // host guarantees divisibility
+    const int per = tiles_m * tiles_n;
+    const int total = per * g.ny * g.nz;
+    const int w = xcd_remap(blockIdx.x, total);
+    const int tile = w % per, yz = w / per;
+    const int y = yz % g.ny, z = yz / g.ny;
+    const int slot = g.slots[z];
+    const int i0 = (tile / tiles_n) * BM, j0 = (tile % tiles_n) * BN;
+    const int gM = g.M, gN = g.N, gK = g.K, lda = g.lda, ldb = g.ldb;
+    const rsrc_t rA = make_rsrc(at(g.A, slot, y), (long long)(gK - 1) * lda + gM);
+    const rsrc_t rB = make_rsrc(at(g.B, slot, y), (long long)(gK - 1) * ldb + gN);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wi = (wave >> 1) * WM, wj = (wave & 1) * WN;
+    const int l32 = lane & 31, lh = lane >> 5;
+    float* bias_s = smem + STAGES * SS;
+    if constexpr (EPI != EPI_STORE) {
+        if (tid < BM) bias_s[tid] = at(g.bias, slot, y)[i0 + tid];
+    }
+
+    const int nk = (gK + BK - 1) / BK;
+#pragma unroll
+    for (int st = 0; st < STAGES - 1; ++st) {
+        const int k0 = (st < nk ? st : nk - 1) * BK;
+        dma_slice<BM, BK>(rA, lda, i0, k0, smem + st * SS, wave, lane);
+        dma_slice<BN, BK>(rB, ldb, j0, k0, smem + st * SS + SA, wave, lane);
+    }
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+    for (int kt = 0; kt < nk; ++kt) {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm((STAGES - 2) * NQ));
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        {
+            const int kn = kt + STAGES - 1;
+            const int k0 = (kn < nk ? kn : nk - 1) * BK;  // past the end: harmless re-load, keeps counts uniform
+            float* dst = smem + (kn % STAGES) * SS;
+            dma_slice<BM, BK>(rA, lda, i0, k0, dst, wave, lane);
+            dma_slice<BN, BK>(rB, ldb, j0, k0, dst + SA, wave, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const float* Ac = smem + (kt % STAGES) * SS;
+        const float* Bc = Ac + SA;
+        float av[BK / 2][TM], bv[BK / 2][TN];
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; ++kk) {
+            const int rr = 2 * kk + lh;
+#pragma unroll
+            for (int a = 0; a < TM; ++a) av[kk][a] = Ac[rr * BM + wi + a * 32 + l32];
+#pragma unroll
+            for (int b = 0; b < TN; ++b) bv[kk][b] = Bc[rr * BN + wj + b * 32 + l32];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < BK / 2; ++kk)
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk][a], bv[kk][b], acc[a][b], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+
+    float* __restrict__ C = at(g.C, slot, y);
+    float* __restrict__ C2 = (EPI == EPI_BIAS_GELU2) ? at(g.C2, slot, y) : nullptr;
+    const int ldc = g.ldc;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+        float bsv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            bsv[r] = (EPI != EPI_STORE) ? bias_s[wi + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh] : 0.f;
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = i0 + wi + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int j = j0 + wj + b * 32 + l32;
+                float v = acc[a][b][r];
+                const long long o = (long long)i * ldc + j;
+                if constexpr (EPI == EPI_STORE) {
+                    C[o] = v;
+                } else if constexpr (EPI == EPI_BIAS) {
+                    C[o] = v + bsv[r];
+                } else if constexpr (EPI == EPI_BIAS_GELU2) {
+                    v += bsv[r];
+                    C[o] = v;
+                    C2[o] = gelu_f(v);
+                } else {
+                    C[o] = gelu_f(v + bsv[r]);
+                }
+            }
+    }
+}
+
+// Register-staged kernel: K slice 32, one accumulator chain.  (BK 64 and dual
+// accumulator chains were measured slower on every shape of the step:
+// profiles/round1_gemm_variants.txt; the template keeps both knobs.)
+template <int BM, int BN, bool ARC, bool BRC, int EPI>
+static void gemm_dispatch_variant(int /*variant*/, dim3 grid, const GemmArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, false, ARC, BRC, EPI>), grid, dim3(256), 0, s, a);
+}
+
+template <int EPI>
+static void gemm_fwd_dma_dispatch(int tile, int stages, const GemmArgs& a, hipStream_t s) {
+    auto grid = [&](int bm, int bn) { return dim3((a.M / bm) * (a.N / bn) * a.ny * a.nz); };
+#define FQ_DMA(BM, BN, ST) hipLaunchKernelGGL((gemm_fwd_dma_kernel<BM, BN, ST, EPI>), grid(BM, BN), dim3(256), 0, s, a)
+    if (tile == 0) {
+        if (stages == 3) FQ_DMA(64, 64, 3);
+        else FQ_DMA(64, 64, 4);
+    } else if (tile == 1) {
+        FQ_DMA(128, 64, 3);
+    } else {
+        FQ_DMA(64, 128, 3);
+    }
+#undef FQ_DMA
+}
+
 template <bool ARC, bool BRC, int EPI>
-static void gemm_dispatch_tile(int tile, const GemmArgs& a, hipStream_t s) {
-    auto grid = [&](int bm, int bn) {
-        return dim3(((a.M + bm - 1) / bm) * (a.N / bn) * a.ny * a.nz);
-    };
+static void gemm_dispatch_tile(int tile, int variant, const GemmArgs& a, hipStream_t s) {
+    if constexpr (!ARC && !BRC) {
+        // variants 4 / 5: LDS-DMA ring with 3 / 4 stages (needs M % BM == 0)
+        if (variant >= 4 && a.M % ((tile & 1) ? 128 : 64) == 0) {
+            gemm_fwd_dma_dispatch<EPI>(tile, variant == 4 ? 3 : 4, a, s);
+            return;
+        }
+    }
+    variant &= 3;
+    auto grid = [&](int bm, int bn) { return dim3(((a.M + bm - 1) / bm) * (a.N / bn) * a.ny * a.nz); };
     switch (tile) {
-        case 0: hipLaunchKernelGGL((gemm_kernel<64, 64, ARC, BRC, EPI>), grid(64, 64), dim3(256), 0, s, a); break;
-        case 1: hipLaunchKernelGGL((gemm_kernel<128, 64, ARC, BRC, EPI>), grid(128, 64), dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((gemm_kernel<64, 128, ARC, BRC, EPI>), grid(64, 128), dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL((gemm_kernel<128, 128, ARC, BRC, EPI>), grid(128, 128), dim3(256), 0, s, a); break;
+        case 0: gemm_dispatch_variant<64, 64, ARC, BRC, EPI>(variant, grid(64, 64), a, s); break;
+        case 1: gemm_dispatch_variant<128, 64, ARC, BRC, EPI>(variant, grid(128, 64), a, s); break;
+        case 2: gemm_dispatch_variant<64, 128, ARC, BRC, EPI>(variant, grid(64, 128), a, s); break;
+        default: gemm_dispatch_variant<128, 128, ARC, BRC, EPI>(variant & 2, grid(128, 128), a, s); break;
+    }
+}
+
+void launch_gemm_variant(int layout, int epi, int tile, int variant, const GemmArgs& a, hipStream_t s) {
+    // column tiles must divide N exactly (no column guard in the kernel)
+    if ((tile & 2) && a.N % 128 != 0) tile &= ~2;
+    if (layout != LAYOUT_FWD) variant &= 3;
+    const int bk = (variant & 1) ? 64 : 32;
+    if (layout != LAYOUT_FWD && a.K % bk != 0) variant &= ~1;  // r-contiguous slices must be whole
+    if (layout == LAYOUT_FWD) {
+        switch (epi) {
+            case EPI_BIAS: gemm_dispatch_tile<false, false, EPI_BIAS>(tile, variant, a, s); break;
+            case EPI_BIAS_GELU2: gemm_dispatch_tile<false, false, EPI_BIAS_GELU2>(tile, variant, a, s); break;
+            default: gemm_dispatch_tile<false, false, EPI_BIAS_GELU>(tile, variant, a, s); break;
+        }
+    } else if (layout == LAYOUT_DX) {
+        gemm_dispatch_tile<true, false, EPI_STORE>(tile, variant, a, s);
+    } else {
+        gemm_dispatch_tile<true, true, EPI_STORE>(tile, variant, a, s);
     }
 }
 
 void launch_gemm(int layout, int epi, int tile, const GemmArgs& a, hipStream_t s) {
-    // column tiles must divide N exactly (no column guard in the kernel)
-    if ((tile & 2) && a.N % 128 != 0) tile &= ~2;
-    if (layout != LAYOUT_FWD && a.K % 32 != 0) {
-        // r-contiguous operands are read in whole 32-wide slices
-        (void)hipErrorInvalidValue;
-        return;
-    }
-    if (layout == LAYOUT_FWD) {
-        switch (epi) {
-            case EPI_BIAS: gemm_dispatch_tile<false, false, EPI_BIAS>(tile, a, s); break;
-            case EPI_BIAS_GELU2: gemm_dispatch_tile<false, false, EPI_BIAS_GELU2>(tile, a, s); break;
-            default: gemm_dispatch_tile<false, false, EPI_BIAS_GELU>(tile, a, s); break;
-        }
-    } else if (layout == LAYOUT_DX) {
-        gemm_dispatch_tile<true, false, EPI_STORE>(tile, a, s);
-    } else {
-        gemm_dispatch_tile<true, true, EPI_STORE>(tile, a, s);
-    }
+    launch_gemm_variant(layout, epi, tile, 0, a, s);
 }
 
 // ================================================= column-reduction kernels ==
@@ -773,17 +955,33 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
     float zn[8], x0[8], zd[8], zm[8], act[8];
     float t, rew, mask;
     const float *obs, *nobs;
+    const uint64_t seed = a.seeds[slot];
+    const uint32_t step = (uint32_t)a.count[slot];
+    // minibatch: injected (packed per active member) or drawn from the dataset
     if (a.inj_batch) {
-        const long long bs = (long long)B * (2 * D + A + 2), ns = (long long)B * (4 * A + 1);
+        const long long bs = (long long)B * (2 * D + A + 2);
         const float* pb = a.inj_batch + z * bs;
-        const float* pn = a.inj_noise + z * ns;
         obs = pb + (long long)b * D;
         const float* pa = pb + (long long)B * D;
         rew = pb[(long long)B * (D + A) + b];
         mask = pb[(long long)B * (D + A + 1) + b];
         nobs = pb + (long long)B * (D + A + 2) + (long long)b * D;
+        for (int j = 0; j < A; ++j) act[j] = pa[b * A + j];
+    } else {
+        uint32_t c[4] = {(uint32_t)b, step, a.stream_salt, 0u};
+        philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        const long long idx = (long long)(((unsigned long long)c[0] * (unsigned long long)a.n_rows) >> 32);
+        for (int j = 0; j < A; ++j) act[j] = a.act[idx * A + j];
+        obs = a.obs + idx * D;
+        nobs = a.nobs + idx * D;
+        rew = a.rew[idx];
+        mask = a.mask[idx];
+    }
+    // noise: injected or drawn on device (Philox keyed by member seed, update count)
+    if (a.inj_noise) {
+        const long long ns = (long long)B * (4 * A + 1);
+        const float* pn = a.inj_noise + z * ns;
         for (int j = 0; j < A; ++j) {
-            act[j] = pa[b * A + j];
             zn[j] = pn[b * A + j];
             x0[j] = pn[(long long)B * A + b * A + j];
             zd[j] = pn[(long long)B * (2 * A + 1) + b * A + j];
@@ -791,11 +989,8 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
         }
         t = pn[(long long)B * 2 * A + b];
     } else {
-        const uint64_t seed = a.seeds[slot];
-        const uint32_t step = (uint32_t)a.count[slot];
         uint32_t c[4] = {(uint32_t)b, step, a.stream_salt, 0u};
         philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-        const long long idx = (long long)(((unsigned long long)c[0] * (unsigned long long)a.n_rows) >> 32);
         t = u01(c[1]);
         float nrm[32];
         philox_normals(nrm, 4 * A, seed, (uint32_t)b, step, a.stream_salt);
@@ -804,12 +999,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
             x0[j] = nrm[A + j];
             zd[j] = nrm[2 * A + j];
             zm[j] = nrm[3 * A + j];
-            act[j] = a.act[idx * A + j];
         }
-        obs = a.obs + idx * D;
-        nobs = a.nobs + idx * D;
-        rew = a.rew[idx];
-        mask = a.mask[idx];
     }
     float* os = at(a.os_in, slot);
     float* bc = at(a.bc_in, slot);

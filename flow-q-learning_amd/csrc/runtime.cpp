@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -157,8 +158,10 @@ struct fqlpop {
     float *inj_batch = nullptr, *inj_noise = nullptr;
     long long inj_bs = 0, inj_ns = 0;
 
-    hipStream_t sM = nullptr, sF = nullptr, sB = nullptr;
+    hipStream_t sM = nullptr, sF = nullptr, sB = nullptr, sX = nullptr;
     hipEvent_t ev_sample, ev_bcfwd, ev_bcloss, ev_flow, ev_bdone, ev_t0, ev_t1;
+    std::vector<hipEvent_t> ev_pool;
+    int ev_next = 0;
     std::map<int, Graphs> graphs;  // key: train*2 + injected
 
     float* alloc(long long per_slot) {
@@ -315,13 +318,35 @@ TRef pref(fqlpop* h, float* arena, const NetLayout& N, long long off) {
     return tref(arena + N.off + off, h->P, N.ens_size);
 }
 
-int pick_tile(int M, int N, int nyz) {
-    // 64x64 gives the most workgroups; use bigger tiles only when the launch
-    // alone has several waves of workgroups for 256 CUs.
-    const long long t64 = (long long)((M + 63) / 64) * ((N + 63) / 64) * nyz;
-    if (t64 >= 2048) return 3;
-    if (t64 >= 1024) return 1;
-    return 0;
+// Fork/join events of one enqueued step come from a pool (a distinct event per
+// record keeps graph capture dependencies unambiguous).
+hipEvent_t next_event(fqlpop* h) {
+    if (h->ev_next >= (int)h->ev_pool.size()) throw FqErr{FQLPOP_E_STATE, "event pool exhausted"};
+    return h->ev_pool[h->ev_next++];
+}
+
+// Tile / pipeline choice per GEMM family, from build/gemm_bench on MI355X
+// (profiles/ records the measurements): forward GEMMs use the LDS-DMA ring
+// (variant 4 = 3 stages, 5 = 4 stages), dX/dW the register-staged kernel.
+struct TileChoice {
+    int tile, variant;
+};
+TileChoice pick_gemm(int layout, int M, int N, int nyz) {
+    const long long t64 = (long long)((M + 63) / 64) * (N / 64) * nyz;
+    if (layout == LAYOUT_FWD) {
+        if (M % 64 != 0) return {0, 0};
+        if (t64 <= 512) return {0, 5};
+        if (N % 128 == 0 && N < 768) return {2, 4};
+        return {0, 4};
+    }
+    if (M < 64) return {0, 0};
+    if (N % 128 != 0) return {0, 0};
+    return {t64 >= 2048 ? 3 : 2, 0};
+}
+
+void gemm(int layout, int epi, const GemmArgs& g, hipStream_t s) {
+    const TileChoice t = pick_gemm(layout, g.M, g.N, g.ny * g.nz);
+    launch_gemm_variant(layout, epi, t.tile, t.variant, g, s);
 }
 
 // Forward of the hidden stack of `N` over `M` columns of input X (ld = ldx).
@@ -347,7 +372,7 @@ void fwd_hidden(const Ctx& c, hipStream_t s, const NetLayout& N, TRef X, int ldx
         g.lda = N.H; g.ldb = ldx; g.ldc = ldx;
         g.ny = N.E; g.nz = c.nz; g.slots = h->slots;
         const int epi = N.ln ? EPI_BIAS : (store_u ? EPI_BIAS_GELU2 : EPI_BIAS_GELU);
-        launch_gemm(LAYOUT_FWD, epi, pick_tile(g.M, g.N, g.ny * g.nz), g, s);
+        gemm(LAYOUT_FWD, epi, g, s);
         if (N.ln) {
             LnArgs a{};
             a.u = tref(U[l], (long long)N.H * ldx * N.E, act_sy);
@@ -382,7 +407,7 @@ HeadArgs head_args(const Ctx& c, const NetLayout& N, float* Glast, int ldx, int 
 void bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_o, TRef X0, int ld,
              long long coff, int M, int Mg, const std::vector<float*>& U, const std::vector<float*>& G,
              long long act_sy, const std::vector<float*>* MU, const std::vector<float*>* RS, long long st_sy,
-             const std::vector<float*>& DU, float* DH, float* C1, float* C2, int ld_d) {
+             const std::vector<float*>& DU, float* DH, float* C1, float* C2, int ld_d, hipStream_t sw) {
     fqlpop* h = c.h;
     const long long act_ss = (long long)N.H * ld * N.E;
     const long long d_ss = (long long)N.H * ld_d * N.E, d_sy = (long long)N.H * ld_d;
@@ -415,7 +440,13 @@ void bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_
         if (N.ln) launch_bwd_rowstats(head, b, s);
         launch_bwd_cols(head, N.ln, b, s);
 
-        // dW_l = X_l^T du_l over the first Mg columns
+        // dW_l = X_l^T du_l over the first Mg columns, on the dW stream `sw`
+        // (off the dX chain's critical path)
+        if (sw != s) {
+            hipEvent_t ev = next_event(h);
+            HIPCHK(hipEventRecord(ev, s));
+            HIPCHK(hipStreamWaitEvent(sw, ev, 0));
+        }
         GemmArgs gw{};
         gw.A = l == 0 ? X0 : act(G[l - 1]);
         gw.B = tref(DU[l], d_ss, d_sy);
@@ -423,7 +454,7 @@ void bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_
         gw.M = N.kdim(l); gw.N = N.H; gw.K = Mg;
         gw.lda = ld; gw.ldb = ld_d; gw.ldc = N.H;
         gw.ny = N.E; gw.nz = c.nz; gw.slots = h->slots;
-        launch_gemm(LAYOUT_DW, EPI_STORE, pick_tile(gw.M, gw.N, gw.ny * gw.nz), gw, s);
+        gemm(LAYOUT_DW, EPI_STORE, gw, sw);
         if (l > 0) {
             // dh_{l-1} = W_l du_l  (all M columns)
             GemmArgs gx{};
@@ -433,7 +464,7 @@ void bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_
             gx.M = N.H; gx.N = M; gx.K = N.H;
             gx.lda = N.H; gx.ldb = ld_d; gx.ldc = ld_d;
             gx.ny = N.E; gx.nz = c.nz; gx.slots = h->slots;
-            launch_gemm(LAYOUT_DX, EPI_STORE, pick_tile(gx.M, gx.N, gx.ny * gx.nz), gx, s);
+            gemm(LAYOUT_DX, EPI_STORE, gx, s);
         }
     }
 }
@@ -457,20 +488,21 @@ void adam_net(const Ctx& c, hipStream_t s, int ni) {
 }
 
 // Enqueue one population update (train) or one total_loss pass (!train).
-void enqueue(fqlpop* h, bool train, bool injected) {
+void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     const Ctx c{h, h->nz};
     const int B = h->B, D = h->D, A = h->A, H = h->H, E = h->E, L = h->L, S = h->S;
     const int Kc = D + A, Kb = D + A + 1;
     const int B2 = 2 * B, B3 = 3 * B;
-    hipStream_t sM = h->sM, sF = h->sF, sB = h->sB;
+    hipStream_t sM = h->sM, sF = h->sF, sB = h->sB, sX = h->sX;
+    h->ev_next = 0;
 
     // ---- sampling / assembly ------------------------------------------
     const auto& dset = (!train && h->ds[1].rows > 0) ? h->ds[1] : h->ds[0];
     SampleArgs sa{};
     sa.obs = dset.obs; sa.act = dset.act; sa.rew = dset.rew; sa.mask = dset.mask; sa.nobs = dset.nobs;
     sa.n_rows = dset.rows;
-    sa.inj_batch = injected ? h->inj_batch : nullptr;
-    sa.inj_noise = injected ? h->inj_noise : nullptr;
+    sa.inj_batch = inj_batch ? h->inj_batch : nullptr;
+    sa.inj_noise = inj_noise ? h->inj_noise : nullptr;
     sa.seeds = h->seeds; sa.count = h->count;
     sa.stream_salt = train ? 0x51A7u : 0x5A1Du;
     sa.B = B; sa.D = D; sa.A = A;
@@ -541,6 +573,13 @@ void enqueue(fqlpop* h, bool train, bool injected) {
         HIPCHK(hipEventRecord(h->ev_flow, sF));
     }
 
+    // Fork / join helper: `to` waits for everything enqueued on `from` so far.
+    auto dep = [&](hipStream_t from, hipStream_t to) {
+        hipEvent_t ev = next_event(h);
+        HIPCHK(hipEventRecord(ev, from));
+        HIPCHK(hipStreamWaitEvent(to, ev, 0));
+    };
+
     // ---- sB: BC loss + backward (+ Adam after the flow chain) ------------
     HIPCHK(hipStreamWaitEvent(sB, h->ev_bcfwd, 0));
     launch_loss_bc(la, sB);
@@ -548,11 +587,11 @@ void enqueue(fqlpop* h, bool train, bool injected) {
     if (train) {
         const NetLayout& N = h->bc;
         bwd_net(c, sB, N, tref(h->dv, (long long)A * B), B, tref(h->bc_in, (long long)Kb * B2), B2, 0, B, B,
-                h->bc_u, h->bc_g, 0, nullptr, nullptr, 0, h->bc_du, h->bc_dh, nullptr, nullptr, B);
+                h->bc_u, h->bc_g, 0, nullptr, nullptr, 0, h->bc_du, h->bc_dh, nullptr, nullptr, B, sB);
         HIPCHK(hipStreamWaitEvent(sB, h->ev_flow, 0));  // Euler reads bc params
         adam_net(c, sB, 1);
-        HIPCHK(hipEventRecord(h->ev_bdone, sB));
     }
+    HIPCHK(hipEventRecord(h->ev_bdone, sB));
 
     // ---- sM: one-step actor forward on [s'; s; s] (z_next; z_d; z_metric) --
     {
@@ -566,17 +605,12 @@ void enqueue(fqlpop* h, bool train, bool injected) {
         ha.o3 = tref(h->amet, (long long)A * B); ha.ld3 = B;
         launch_head_fwd(HEAD_OS, ha, sM);
     }
-    // ---- critic on [s,a ; s,clip(a_pi)] and target critic on [s', a'] ----
+    dep(sM, sX);  // a' is in the target-critic input
+    const NetLayout& NC = h->critic;
+    const long long sy2 = (long long)H * B2, sy1 = (long long)H * B;
+    // ---- sX: target critic on [s', a'] (params from the target arena) -----
     {
-        const NetLayout& N = h->critic;
-        const long long sy2 = (long long)H * B2, sy1 = (long long)H * B;
-        fwd_hidden(c, sM, N, tref(h->cr_in, (long long)Kc * B2, 0), B2, B2, h->cr_u, h->cr_h, sy2,
-                   &h->cr_mu, &h->cr_rs, B2, true);
-        HeadArgs hc = head_args(c, N, h->cr_h[L - 1], B2, B2, sy2);
-        hc.o0 = tref(h->q, (long long)E * B2, B2); hc.ld0 = B2;
-        launch_head_fwd(HEAD_STORE, hc, sM);
-
-        // target critic: same layout, params from the target arena
+        const NetLayout& N = NC;
         for (int l = 0; l < L; ++l) {
             GemmArgs g{};
             g.A = tref(h->target + N.W[l], h->PT, N.ens_size);
@@ -586,7 +620,7 @@ void enqueue(fqlpop* h, bool train, bool injected) {
             g.M = H; g.N = B; g.K = N.kdim(l);
             g.lda = H; g.ldb = B; g.ldc = B;
             g.ny = E; g.nz = c.nz; g.slots = h->slots;
-            launch_gemm(LAYOUT_FWD, N.ln ? EPI_BIAS : EPI_BIAS_GELU, pick_tile(g.M, g.N, g.ny * g.nz), g, sM);
+            gemm(LAYOUT_FWD, N.ln ? EPI_BIAS : EPI_BIAS_GELU, g, sX);
             if (N.ln) {
                 LnArgs a{};
                 a.u = tref(h->tg_u[l], (long long)H * B * E, sy1);
@@ -596,7 +630,7 @@ void enqueue(fqlpop* h, bool train, bool injected) {
                 a.gamma = tref(h->target + N.gam[l], h->PT, N.ens_size);
                 a.beta = tref(h->target + N.bet[l], h->PT, N.ens_size);
                 a.H = H; a.M = B; a.ld = B; a.ny = E; a.nz = c.nz; a.slots = h->slots;
-                launch_ln_gelu_fwd(a, sM);
+                launch_ln_gelu_fwd(a, sX);
             }
         }
         HeadArgs ht{};
@@ -606,22 +640,34 @@ void enqueue(fqlpop* h, bool train, bool injected) {
         ht.H = H; ht.M = B; ht.ld = B; ht.nout = 1; ht.B = B; ht.D = D; ht.steps_f = (float)S;
         ht.o0 = tref(h->qt, (long long)E * B, B); ht.ld0 = B;
         ht.ny = E; ht.nz = c.nz; ht.slots = h->slots;
-        launch_head_fwd(HEAD_STORE, ht, sM);
+        launch_head_fwd(HEAD_STORE, ht, sX);
     }
+    // ---- sM: critic on [s,a ; s,clip(a_pi)] -------------------------------
+    {
+        const NetLayout& N = NC;
+        fwd_hidden(c, sM, N, tref(h->cr_in, (long long)Kc * B2, 0), B2, B2, h->cr_u, h->cr_h, sy2,
+                   &h->cr_mu, &h->cr_rs, B2, true);
+        HeadArgs hc = head_args(c, N, h->cr_h[L - 1], B2, B2, sy2);
+        hc.o0 = tref(h->q, (long long)E * B2, B2); hc.ld0 = B2;
+        launch_head_fwd(HEAD_STORE, hc, sM);
+    }
+    dep(sX, sM);  // Q_target
     launch_loss_critic(la, sM);
     if (train) {
-        const NetLayout& N = h->critic;
-        const long long sy2 = (long long)H * B2;
-        bwd_net(c, sM, N, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0), B2, 0,
-                B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, h->cr_dh, h->cr_c1, h->cr_c2, B2);
+        // critic backward: the dX chain stays on sM, the dW GEMMs go to sX
+        bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0), B2, 0,
+                B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, h->cr_dh, h->cr_c1, h->cr_c2, B2,
+                sX);
         InGradArgs ig{};
-        ig.W0 = pref(h, h->params, N, N.W[0]);
+        ig.W0 = pref(h, h->params, NC, NC.W[0]);
         ig.du0 = tref(h->cr_du[0], (long long)H * B2 * E, sy2);
         ig.da = tref(h->da, (long long)A * B);
         ig.H = H; ig.D = D; ig.A = A; ig.E = E; ig.ld = B2; ig.off = B; ig.M = B;
         ig.nz = c.nz; ig.slots = h->slots;
         launch_input_grad(ig, sM);
-        adam_net(c, sM, 0);  // critic Adam + target EMA (all critic reads of this step are done)
+        // critic Adam + target EMA once every read of the critic params is done
+        dep(sM, sX);
+        adam_net(c, sX, 0);
     }
     HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
     HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
@@ -629,8 +675,10 @@ void enqueue(fqlpop* h, bool train, bool injected) {
     if (train) {
         const NetLayout& N = h->os;
         bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3, B, B, B,
-                h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, h->os_dh, nullptr, nullptr, B);
-        adam_net(c, sM, 2);
+                h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, h->os_dh, nullptr, nullptr, B, sX);
+        dep(sM, sX);
+        adam_net(c, sX, 2);
+        dep(sX, sM);
         HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
         FinalArgs fa{};
         fa.stats = h->stats; fa.chunk_leaf = h->chunk_leaf;
@@ -640,18 +688,20 @@ void enqueue(fqlpop* h, bool train, bool injected) {
         fa.nz = c.nz; fa.slots = h->slots;
         launch_finalize(fa, sM);
     } else {
-        HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
+        HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
     }
     HIPCHK(hipGetLastError());
 }
 
-void run(fqlpop* h, bool train, bool injected) {
+void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     if (h->nz == 0) return;
     if (!h->cfg.use_graph) {
-        enqueue(h, train, injected);
+        enqueue(h, train, inj_batch, inj_noise);
         return;
     }
-    const int key = (train ? 2 : 0) + (injected ? 1 : 0);
+    // one graph per (mode, active-member count): kernels read the active slot ids
+    // from device memory, so any active set of the same size replays the graph
+    const int key = ((train ? 4 : 0) + (inj_batch ? 2 : 0) + (inj_noise ? 1 : 0)) + 8 * h->nz;
     Graphs& gr = h->graphs[key];
     if (gr.exec == nullptr || gr.nz != h->nz) {
         if (gr.exec) HIPCHK(hipGraphExecDestroy(gr.exec));
@@ -659,7 +709,7 @@ void run(fqlpop* h, bool train, bool injected) {
         hipGraph_t graph;
         HIPCHK(hipStreamBeginCapture(h->sM, hipStreamCaptureModeRelaxed));
         try {
-            enqueue(h, train, injected);
+            enqueue(h, train, inj_batch, inj_noise);
         } catch (...) {
             (void)hipStreamEndCapture(h->sM, &graph);
             throw;
@@ -757,6 +807,16 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         HIPCHK(hipStreamCreateWithFlags(&h->sM, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&h->sF, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
+        // A 4th stream (target critic + dW GEMMs + Adams off the main chain) is
+        // opt-in: on MI355X the step is throughput-bound and the extra
+        // concurrency measured 5% slower (profiles/round1_notes.md).
+        {
+            const char* ns = std::getenv("FQLPOP_STREAMS");
+            if (ns && std::atoi(ns) >= 4) HIPCHK(hipStreamCreateWithFlags(&h->sX, hipStreamNonBlocking));
+            else h->sX = h->sM;
+        }
+        h->ev_pool.resize(64);
+        for (auto& e : h->ev_pool) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         for (hipEvent_t* e : {&h->ev_sample, &h->ev_bcfwd, &h->ev_bcloss, &h->ev_flow, &h->ev_bdone})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         HIPCHK(hipEventCreate(&h->ev_t0));
@@ -849,6 +909,8 @@ int fqlpop_destroy(fqlpop_t* h) {
                 if (p) (void)hipFree(p);
         for (hipEvent_t e : {h->ev_sample, h->ev_bcfwd, h->ev_bcloss, h->ev_flow, h->ev_bdone, h->ev_t0, h->ev_t1})
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+        if (h->sX && h->sX != h->sM) (void)hipStreamDestroy(h->sX);
         for (hipStream_t s : {h->sM, h->sF, h->sB})
             if (s) (void)hipStreamDestroy(s);
         delete h;
@@ -898,18 +960,25 @@ int fqlpop_step(fqlpop_t* h, int n_steps) {
         ARGCHK(n_steps >= 0, "n_steps must be >= 0");
         if (h->ds[0].rows == 0) throw FqErr{FQLPOP_E_STATE, "no training dataset set (fqlpop_set_dataset)"};
         HIPCHK(hipSetDevice(h->device));
-        for (int i = 0; i < n_steps; ++i) run(h, true, false);
+        for (int i = 0; i < n_steps; ++i) run(h, true, false, false);
     });
+}
+
+// stage the injected batch / noise of every active member on sM
+static void stage_injected(fqlpop* h, const float* batch, const float* noise) {
+    if (batch)
+        HIPCHK(hipMemcpyAsync(h->inj_batch, batch, sizeof(float) * h->inj_bs * h->nz, hipMemcpyHostToDevice, h->sM));
+    if (noise)
+        HIPCHK(hipMemcpyAsync(h->inj_noise, noise, sizeof(float) * h->inj_ns * h->nz, hipMemcpyHostToDevice, h->sM));
 }
 
 int fqlpop_step_injected(fqlpop_t* h, const float* batch, const float* noise) {
     return guard([&] {
-        ARGCHK(h && batch && noise, "null argument");
+        ARGCHK(h && batch, "null argument");
         HIPCHK(hipSetDevice(h->device));
         if (h->nz == 0) return;
-        HIPCHK(hipMemcpyAsync(h->inj_batch, batch, sizeof(float) * h->inj_bs * h->nz, hipMemcpyHostToDevice, h->sM));
-        HIPCHK(hipMemcpyAsync(h->inj_noise, noise, sizeof(float) * h->inj_ns * h->nz, hipMemcpyHostToDevice, h->sM));
-        run(h, true, true);
+        stage_injected(h, batch, noise);
+        run(h, true, true, noise != nullptr);
         HIPCHK(hipStreamSynchronize(h->sM));  // host buffers are borrowed only for the call
     });
 }
@@ -917,18 +986,13 @@ int fqlpop_step_injected(fqlpop_t* h, const float* batch, const float* noise) {
 int fqlpop_total_loss(fqlpop_t* h, const float* batch, const float* noise) {
     return guard([&] {
         ARGCHK(h, "null handle");
-        ARGCHK((batch == nullptr) == (noise == nullptr), "batch and noise must both be given or both NULL");
+        ARGCHK(batch != nullptr || noise == nullptr, "noise without batch is not supported");
         HIPCHK(hipSetDevice(h->device));
         if (h->nz == 0) return;
-        const bool inj = batch != nullptr;
-        if (!inj && h->ds[0].rows == 0 && h->ds[1].rows == 0)
-            throw FqErr{FQLPOP_E_STATE, "no dataset set"};
-        if (inj) {
-            HIPCHK(hipMemcpyAsync(h->inj_batch, batch, sizeof(float) * h->inj_bs * h->nz, hipMemcpyHostToDevice, h->sM));
-            HIPCHK(hipMemcpyAsync(h->inj_noise, noise, sizeof(float) * h->inj_ns * h->nz, hipMemcpyHostToDevice, h->sM));
-        }
-        run(h, false, inj);
-        if (inj) HIPCHK(hipStreamSynchronize(h->sM));
+        if (!batch && h->ds[0].rows == 0 && h->ds[1].rows == 0) throw FqErr{FQLPOP_E_STATE, "no dataset set"};
+        stage_injected(h, batch, noise);
+        run(h, false, batch != nullptr, noise != nullptr);
+        if (batch) HIPCHK(hipStreamSynchronize(h->sM));
     });
 }
 
@@ -995,7 +1059,7 @@ int fqlpop_sample_actions(fqlpop_t* h, int member, const float* obs, int64_t n, 
             if (N.ln) {
                 throw FqErr{FQLPOP_E_UNSUPPORTED, "sample_actions with actor_layer_norm is not supported"};
             }
-            launch_gemm(LAYOUT_FWD, EPI_BIAS_GELU, 0, g, h->sM);
+            gemm(LAYOUT_FWD, EPI_BIAS_GELU, g, h->sM);
         }
         HeadArgs ha{};
         ha.h = tref(buf[(L - 1) & 1], 0);
@@ -1131,6 +1195,7 @@ int fqlpop_sync(fqlpop_t* h) {
         HIPCHK(hipStreamSynchronize(h->sM));
         HIPCHK(hipStreamSynchronize(h->sF));
         HIPCHK(hipStreamSynchronize(h->sB));
+        if (h->sX != h->sM) HIPCHK(hipStreamSynchronize(h->sX));
     });
 }
 
@@ -1149,10 +1214,9 @@ int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* 
         g.bias = pref(h, h->params, N, N.b[1]);
         g.M = H; g.N = B; g.K = H; g.lda = H; g.ldb = B; g.ldc = B;
         g.ny = 1; g.nz = h->nz; g.slots = h->slots;
-        const int tile = pick_tile(g.M, g.N, g.nz);
-        launch_gemm(LAYOUT_FWD, EPI_BIAS_GELU, tile, g, h->sF);  // warm-up
+        gemm(LAYOUT_FWD, EPI_BIAS_GELU, g, h->sF);  // warm-up
         HIPCHK(hipEventRecord(h->ev_t0, h->sF));
-        for (int i = 0; i < iters; ++i) launch_gemm(LAYOUT_FWD, EPI_BIAS_GELU, tile, g, h->sF);
+        for (int i = 0; i < iters; ++i) gemm(LAYOUT_FWD, EPI_BIAS_GELU, g, h->sF);
         HIPCHK(hipEventRecord(h->ev_t1, h->sF));
         HIPCHK(hipEventSynchronize(h->ev_t1));
         float ms = 0.f;

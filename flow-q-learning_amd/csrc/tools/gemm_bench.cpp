@@ -47,6 +47,25 @@ __global__ void fill(float* p, long long n, unsigned seed) {
     p[i] = ((x & 0xFFFFFF) / 16777216.0f - 0.5f);
 }
 
+// pure MFMA issue loop: registers only, random operands, NACC independent chains
+template <int NACC>
+__global__ __launch_bounds__(256) void mfma_peak(float* out, int iters, float seed) {
+    typedef float f16v __attribute__((ext_vector_type(16)));
+    f16v acc[NACC];
+    for (int c = 0; c < NACC; ++c)
+        for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+    float a = seed * (threadIdx.x + 1) * 1e-3f, b = seed * (blockIdx.x + 3) * 1e-3f;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int c = 0; c < NACC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[c], 0, 0, 0);
+        a += 1e-7f;
+    }
+    float s = 0.f;
+    for (int c = 0; c < NACC; ++c)
+        for (int r = 0; r < 16; ++r) s += acc[c][r];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 struct Shape {
     const char* name;
     int layout, M, N, K, ny;
@@ -81,7 +100,25 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&slots, sizeof(int) * nz));
     CK(hipMemcpy(slots, hs.data(), sizeof(int) * nz, hipMemcpyHostToDevice));
 
-    std::printf("%-28s %5s %10s %10s %9s\n", "shape", "tile", "us", "TFLOP/s", "maxerr");
+    {
+        float* o;
+        CK(hipMalloc(&o, sizeof(float) * 256 * 4096));
+        for (int wgs : {256, 512, 1024}) {
+            const int it = 4000;
+            hipLaunchKernelGGL(mfma_peak<2>, dim3(wgs), dim3(256), 0, s, o, it, 0.37f);
+            CK(hipEventRecord(e0, s));
+            hipLaunchKernelGGL(mfma_peak<2>, dim3(wgs), dim3(256), 0, s, o, it, 0.37f);
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            const double fl = 2.0 * 32 * 32 * 2 * 2.0 * it * 4 * wgs;
+            std::printf("mfma_f32_32x32x2 peak loop: %d WGs x 4 waves x 2 chains: %.1f TFLOP/s (%.2f ms)\n", wgs,
+                        fl / (ms * 1e-3) / 1e12, ms);
+        }
+        CK(hipFree(o));
+    }
+    std::printf("%-28s %5s %10s %10s %9s\n", "shape", "t/var", "us", "TFLOP/s", "maxerr");
     for (const Shape& sh : shapes) {
         const bool arc = sh.layout != LAYOUT_FWD, brc = sh.layout == LAYOUT_DW;
         // operand extents: A is (i x r) or (r x i) etc; allocate generously
@@ -104,7 +141,10 @@ int main(int argc, char** argv) {
         CK(hipStreamSynchronize(s));
         std::vector<float> hr((size_t)szC * nb), hc((size_t)szC * nb);
         CK(hipMemcpy(hr.data(), R, sizeof(float) * szC * nb, hipMemcpyDeviceToHost));
-        for (int tile = 0; tile < 4; ++tile) {
+        const int tvs[][2] = {{0, 0}, {1, 0}, {2, 0}, {3, 0}, {0, 4}, {1, 4}, {2, 4}, {0, 5}};
+        for (const auto& tv : tvs) {
+            const int tile = tv[0], variant = tv[1];
+            if (variant >= 4 && sh.layout != LAYOUT_FWD) continue;
             GemmArgs g{};
             g.A = tref(A, szA * sh.ny, szA);
             g.B = tref(B, szB * sh.ny, szB);
@@ -114,7 +154,7 @@ int main(int argc, char** argv) {
             g.ny = sh.ny; g.nz = nz; g.slots = slots;
             const int epi = sh.layout == LAYOUT_FWD ? EPI_BIAS : EPI_STORE;
             CK(hipMemset(C, 0, sizeof(float) * szC * nb));
-            launch_gemm(sh.layout, epi, tile, g, s);
+            launch_gemm_variant(sh.layout, epi, tile, variant, g, s);
             CK(hipStreamSynchronize(s));
             CK(hipMemcpy(hc.data(), C, sizeof(float) * szC * nb, hipMemcpyDeviceToHost));
             double maxerr = 0;
@@ -125,14 +165,14 @@ int main(int argc, char** argv) {
                         maxerr = std::max(maxerr, (double)std::fabs(hc[o] - hr[o]));
                     }
             CK(hipEventRecord(e0, s));
-            for (int it = 0; it < iters; ++it) launch_gemm(sh.layout, epi, tile, g, s);
+            for (int it = 0; it < iters; ++it) launch_gemm_variant(sh.layout, epi, tile, variant, g, s);
             CK(hipEventRecord(e1, s));
             CK(hipEventSynchronize(e1));
             float ms;
             CK(hipEventElapsedTime(&ms, e0, e1));
             const double us = 1000.0 * ms / iters;
             const double fl = 2.0 * sh.M * sh.N * (double)sh.K * nb;
-            std::printf("%-28s %5d %10.2f %10.2f %9.2e\n", sh.name, tile, us, fl / us / 1e6, maxerr);
+            std::printf("%-28s %3d/%d %10.2f %10.2f %9.2e\n", sh.name, tile, variant, us, fl / us / 1e6, maxerr);
         }
         CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R)); CK(hipFree(bias));
     }

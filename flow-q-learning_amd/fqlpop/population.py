@@ -172,35 +172,54 @@ class Population:
         """n_steps population updates (device-side sampling) of every active member."""
         check(self.lib.fqlpop_step(self._h, int(n_steps)))
 
-    def _pack(self, batches, noises):
+    def _pack_batches(self, batches):
         B = self.cfg.batch_size
         D, A = self.cfg.obs_dim, self.cfg.action_dim
-        pb, pn = [], []
-        for b, nz in zip(batches, noises):
-            pb += [_f32(b["observations"]).reshape(B * D), _f32(b["actions"]).reshape(B * A),
-                   _f32(b["rewards"]).reshape(B), _f32(b["masks"]).reshape(B),
-                   _f32(b["next_observations"]).reshape(B * D)]
-            pn += [_f32(nz["z_next"]).reshape(B * A), _f32(nz["x0"]).reshape(B * A),
-                   _f32(nz["t"]).reshape(B), _f32(nz["z_d"]).reshape(B * A),
-                   _f32(nz["z_metric"]).reshape(B * A)]
-        return np.concatenate(pb), np.concatenate(pn)
+        parts = []
+        for b in batches:
+            parts += [_f32(b["observations"]).reshape(B * D), _f32(b["actions"]).reshape(B * A),
+                      _f32(b["rewards"]).reshape(B), _f32(b["masks"]).reshape(B),
+                      _f32(b["next_observations"]).reshape(B * D)]
+        return np.concatenate(parts)
 
-    def step_injected(self, batches, noises):
-        """One update of every active member (in slot order) on the given batch
-        and noise dicts (parity mode, see oracle/fql_oracle.py)."""
-        ids = self.active_ids
-        if len(batches) != len(ids) or len(noises) != len(ids):
-            raise ValueError("one batch and one noise dict per active member")
-        pb, pn = self._pack(batches, noises)
-        check(self.lib.fqlpop_step_injected(self._h, fptr(pb), fptr(pn)))
+    def _pack_noises(self, noises):
+        if noises is None:
+            return None
+        B, A = self.cfg.batch_size, self.cfg.action_dim
+        parts = []
+        for nz in noises:
+            parts += [_f32(nz["z_next"]).reshape(B * A), _f32(nz["x0"]).reshape(B * A),
+                      _f32(nz["t"]).reshape(B), _f32(nz["z_d"]).reshape(B * A),
+                      _f32(nz["z_metric"]).reshape(B * A)]
+        return np.concatenate(parts)
+
+    def _check_count(self, items, what):
+        if items is not None and len(items) != len(self.active_ids):
+            raise ValueError(f"one {what} per active member ({len(self.active_ids)}), got {len(items)}")
+
+    def step_injected(self, batches, noises=None):
+        """One update of every active member (in slot order) on the given host
+        batches.  ``noises`` None: drawn on device; else the parity mode (see
+        oracle/fql_oracle.py for the keys)."""
+        self._check_count(batches, "batch")
+        self._check_count(noises, "noise dict")
+        pb = self._pack_batches(batches)
+        pn = self._pack_noises(noises)
+        check(self.lib.fqlpop_step_injected(self._h, fptr(pb), None if pn is None else fptr(pn)))
 
     def total_loss(self, batches=None, noises=None):
-        """Validation losses of every active member; returns {member: info}."""
+        """Validation losses of every active member; returns {member: info}.
+        ``batches`` None: sampled on device from the val dataset."""
         if batches is None:
+            if noises is not None:
+                raise ValueError("noises need batches")
             check(self.lib.fqlpop_total_loss(self._h, None, None))
         else:
-            pb, pn = self._pack(batches, noises)
-            check(self.lib.fqlpop_total_loss(self._h, fptr(pb), fptr(pn)))
+            self._check_count(batches, "batch")
+            self._check_count(noises, "noise dict")
+            pb = self._pack_batches(batches)
+            pn = self._pack_noises(noises)
+            check(self.lib.fqlpop_total_loss(self._h, fptr(pb), None if pn is None else fptr(pn)))
         return self.read_info("val")
 
     def read_info_array(self, which: str = "train") -> np.ndarray:

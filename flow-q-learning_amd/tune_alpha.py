@@ -1,0 +1,91 @@
+"""alpha-sweep driver (reference tune_alpha.py:14-95), same flags and flow:
+alpha = logspace(log10 3, log10 1000, --number_of_alphas), seeds =
+random.sample(range(10000), --number_of_seeds) after random.seed(--seed);
+--single_experiment --job_id=i runs one (alpha, seed) to completion with a
+checkpoint every eval_interval; otherwise an Identity-strategy Trainer trains
+the whole population (here: all members together on the GPU) and writes
+<save>/<env>/checkpoint.pkl.  --strategy successive_halving selects halving.
+
+Data: --task synthetic (default; SURVEY.md 8d transitions + a toy evaluation
+env) or --task npz (local OGBench .npz files under --data_directory).
+"""
+from __future__ import annotations
+
+import itertools
+import os
+import pickle
+import random
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from argparser import build_config_from_args, get_argparser  # noqa: E402
+from hpo.identity import Identity  # noqa: E402
+from hpo.successive_halving import SuccessiveHalving  # noqa: E402
+from trainer.config import ExperimentConfig  # noqa: E402
+from trainer.experiment import Experiment  # noqa: E402
+from trainer.trainer import Trainer  # noqa: E402
+
+
+def make_task(args, config):
+    if args.task == "npz":
+        from task.offline_task_npz import OfflineTaskNpz
+        return OfflineTaskNpz(config.env_name, config.data_directory)
+    from task.offline_task_synthetic import OfflineTaskSynthetic
+    return OfflineTaskSynthetic(config.env_name, n_rows=args.synthetic_rows,
+                                num_evaluation_envs=min(config.eval_episodes, 64), seed=config.seed)
+
+
+def main(argv=None):
+    parser = get_argparser()
+    parser.add_argument("--max_evaluations", type=int, default=200)
+    parser.add_argument("--number_of_seeds", type=int, default=1)
+    parser.add_argument("--number_of_alphas", type=int, default=1)
+    parser.add_argument("--task", choices=("synthetic", "npz"), default="synthetic")
+    parser.add_argument("--synthetic_rows", type=int, default=100_000)
+    parser.add_argument("--strategy", choices=("identity", "successive_halving"), default="identity")
+    parser.add_argument("--fraction", type=float, default=0.5)
+    parser.add_argument("--history_length", type=int, default=1)
+    args = parser.parse_args(argv)
+    config = build_config_from_args(args)
+
+    random.seed(config.seed)
+    np.random.seed(config.seed)
+    alpha_values = np.logspace(np.log10(3), np.log10(1000), num=args.number_of_alphas).tolist()
+    seeds = random.sample(range(10000), args.number_of_seeds)
+    combinations = list(itertools.product(alpha_values, seeds))
+    task = make_task(args, config)
+
+    if args.single_experiment:
+        alpha, seed = combinations[args.job_id]
+        experiment = Experiment(task, config, ExperimentConfig(seed=seed, alpha=alpha))
+        done = False
+        while not done:
+            done = experiment.train(config.eval_interval)
+            experiment.save_agent(checkpoint=True)
+        experiment.stop()
+        return
+
+    configs = [ExperimentConfig(seed=seed, alpha=alpha) for alpha, seed in combinations]
+    ckpt = config.save_directory / config.env_name / "checkpoint.pkl"
+    state = {}
+    if ckpt.exists():
+        with open(ckpt, "rb") as f:  # written by this script
+            state = pickle.load(f)
+    if args.strategy == "identity":
+        strategy = Identity(population=configs, total_evaluations=0, state_dict=state.get("strategy"))
+    else:
+        strategy = SuccessiveHalving(population=set(configs), total_evaluations=args.max_evaluations,
+                                     fraction=args.fraction, history_length=args.history_length,
+                                     state_dict=state.get("strategy"))
+    trainer = Trainer(task, strategy, config, state_dict=state.get("trainer"))
+    trainer.train(max_evaluations=args.max_evaluations)
+    ckpt.parent.mkdir(parents=True, exist_ok=True)
+    with open(ckpt, "wb") as f:
+        pickle.dump({"trainer": trainer.state_dict(), "strategy": trainer.strategy.state_dict()}, f)
+
+
+if __name__ == "__main__":
+    main()

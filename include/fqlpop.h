@@ -104,17 +104,19 @@ int fqlpop_set_active(fqlpop_t* h, const uint8_t* mask);
  * seed and update count) and run agent.update(batch) [EXT FQLAgent.update]. */
 int fqlpop_step(fqlpop_t* h, int n_steps);
 
-/* Parity mode of agent.update(batch): one update of every active member on
- * injected data.  batch: per active member (in slot order) the row-major
- * block [obs B*D][act B*A][rew B][mask B][next_obs B*D]; noise: per active
- * member [z_next B*A][x0 B*A][t B][z_d B*A][z_metric B*A].  Host pointers. */
+/* agent.update(batch) (trainer/experiment.py:109) on a host batch: one
+ * update of every active member.  batch: per active member (in slot order)
+ * the row-major block [obs B*D][act B*A][rew B][mask B][next_obs B*D].
+ * noise: NULL => drawn on device (Philox keyed by member seed and update
+ * count); else the parity mode: per active member
+ * [z_next B*A][x0 B*A][t B][z_d B*A][z_metric B*A].  Host pointers. */
 int fqlpop_step_injected(fqlpop_t* h, const float* batch, const float* noise);
 
 /* Replaces agent.total_loss(val_batch, grad_params=None)
  * (trainer/experiment.py:114-115): losses of every active member, no update.
- * batch/noise NULL => sample from the val dataset (which = 1, or the train
- * dataset if no val dataset was set) with device RNG; else injected as in
- * fqlpop_step_injected. Results via fqlpop_read_info(h, 1, ...). */
+ * batch NULL => sample from the val dataset (which = 1, or the train
+ * dataset if no val dataset was set); noise NULL => device RNG; else
+ * injected as in fqlpop_step_injected. Results via fqlpop_read_info(h, 1, .). */
 int fqlpop_total_loss(fqlpop_t* h, const float* batch, const float* noise);
 
 /* Copies info[n_members][FQLPOP_INFO_STRIDE] of the last train step (which=0)

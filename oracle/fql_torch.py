@@ -155,7 +155,7 @@ class TorchFQL:
                     p.sub_(cfg.lr * (m / bc1) / (torch.sqrt(v / bc2) + 1e-8))
             for k, tp in self.P["target_critic"].items():
                 tp.mul_(1 - cfg.tau).add_(old_critic[k], alpha=cfg.tau)
-        return {k: float(v) for k, v in info.items()}
+        return {k: float(v.detach()) if hasattr(v, 'detach') else float(v) for k, v in info.items()}
 
 
 def grads_autograd(cfg: OracleConfig, params: dict, batch: dict, noise: dict):
@@ -172,7 +172,7 @@ def grads_autograd(cfg: OracleConfig, params: dict, batch: dict, noise: dict):
     for net in NETS:
         out[net] = {k: (v.grad.numpy() if v.grad is not None else torch.zeros_like(v).numpy())
                     for k, v in P[net].items()}
-    return float(loss), {k: float(v) for k, v in info.items()}, out
+    return float(loss.detach()), {k: float(v.detach()) for k, v in info.items()}, out
 
 
 __all__ = ["TorchFQL", "grads_autograd", "total_loss", "net_has_ln"]
