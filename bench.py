@@ -109,6 +109,11 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=100)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_dominant.json"),
+                    help="HBM bytes per dominant-kernel launch measured by rocprofv3 --pmc passes "
+                         "(csrc/tools/pmc_summary.py output); missing file -> traffic null")
+    ap.add_argument("--no-probe", action="store_true",
+                    help="time the step without the in-step timing nodes of the dominant kernel")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -143,6 +148,9 @@ def main():
     log(f"[rank {rank}] warmup {args.warmup} steps, {pop.n} members")
     pop.step(args.warmup)
     pop.sync()
+    # every launch of the dominant kernel inside the timed steps stamps its
+    # blocks' start/end (s_memrealtime); read_probe() reduces them per launch
+    pop.set_probe(not args.no_probe)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -159,6 +167,8 @@ def main():
     if distributed:
         dist.barrier()
     el = D.max_over_ranks(el, dev)
+    probe_us, probe_n, _ = pop.read_probe()
+    pop.set_probe(False)
     info = pop.read_info_array()
     finite = bool(np.all(np.isfinite(info[:, :13])))
 
@@ -166,9 +176,21 @@ def main():
     value = member_steps / el
     flops_ms = pop.flops_per_member_step
 
-    # dominant kernel: hidden-layer forward GEMM of the Euler flow (all members, one launch)
-    avg_us, kflops = pop.time_dominant_kernel(args.kernel_iters)
-    achieved = kflops / (avg_us * 1e-6) / 1e12
+    # dominant kernel: Euler-flow hidden-layer forward GEMM (all members, one launch)
+    kflops = pop.dominant_kernel_flops()
+    iso_us, _ = pop.time_dominant_kernel(args.kernel_iters)  # the same launch replayed alone
+    _, _, (cc_event_us, cc_stamp_us) = pop.read_probe()     # stamp clock vs HIP events, one launch
+    launch_us = probe_us if probe_n else iso_us
+    achieved = kflops / (launch_us * 1e-6) / 1e12
+    # algorithmic bytes of one launch: W (H x H) + x' (H x B) + bias read, y' (H x B) written, per member
+    H, B = pcfg.hidden_dims[0], pcfg.batch_size
+    kbytes = 4.0 * (H * H + H * B + H + H * B) * pop.n
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        with open(args.pmc_json) as f:
+            pmc = json.load(f)
+        if pmc.get("kernel_regex") and pmc.get("members") == pop.n:
+            traffic = pmc["traffic_bytes_per_launch"]
 
     result = {
         "metric": "FQL grad-steps/sec (whole node) over 16-alpha population, cube-single-v0"
@@ -199,14 +221,20 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "gemm_kernel<fwd, bias+gelu> (Euler-flow hidden layer, 512x512 @ 512xB per member)",
+            "kernel": "gemm_fwd_dma_kernel<64, 64, 4, 3, 1> (Euler-flow hidden layer: y' = gelu(W^T x' + b), "
+                      "512x512 @ 512x256 per member, 16 members per launch)",
             "achieved": round(achieved, 3),
             "peak": MI355X_FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / MI355X_FP32_MFMA_PEAK_TFLOPS, 4),
-            "avg_launch_us": round(avg_us, 3),
+            "avg_launch_us": round(launch_us, 3),
+            "launches_timed": probe_n,
+            "isolated_launch_us": round(iso_us, 3),
+            "timing": "in-step launches timed by per-block s_memrealtime stamps (100 MHz); cross-check on one "
+                      f"isolated launch: HIP events {cc_event_us:.2f} us vs stamps {cc_stamp_us:.2f} us",
             "flops_per_launch": kflops,
-            "traffic": None,
+            "algorithmic_bytes_per_launch": kbytes,
+            "traffic": traffic,
         },
         "cpu_baseline": None,
     }

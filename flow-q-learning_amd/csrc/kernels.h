@@ -36,9 +36,16 @@ struct GemmArgs {
     int lda, ldb, ldc;
     int ny, nz;
     const int* slots;
+    // optional timing probe (dominant kernel only): per block {start, end}
+    // s_memrealtime stamps (100 MHz), [2 * blockIdx.x + 0/1]
+    unsigned long long* probe;
 };
 // tile: 0 = 64x64, 1 = 128x64 (i x j), 2 = 64x128, 3 = 128x128
 void launch_gemm(int layout, int epi, int tile, const GemmArgs& a, hipStream_t s);
+// The dominant kernel of the step: Euler-flow hidden layer, forward GEMM with
+// bias+GELU epilogue on the 4-stage LDS-DMA ring (its own kernel symbol).
+// Requires M % 64 == 0 and N % 64 == 0.
+void launch_gemm_euler_hidden(const GemmArgs& a, hipStream_t s);
 // variant: bit 0 = K slice 64 (else 32), bit 1 = two accumulator chains
 void launch_gemm_variant(int layout, int epi, int tile, int variant, const GemmArgs& a, hipStream_t s);
 

@@ -162,6 +162,22 @@ struct fqlpop {
     hipEvent_t ev_sample, ev_bcfwd, ev_bcloss, ev_flow, ev_bdone, ev_t0, ev_t1;
     std::vector<hipEvent_t> ev_pool;
     int ev_next = 0;
+    // in-step timing probe of the dominant kernel (Euler hidden-layer GEMM):
+    // its blocks stamp s_memrealtime into per-launch slots; two slot sets are
+    // used by alternate steps so the host reads step i-2 while step i runs
+    bool probe = false;
+    int probe_set = -1;            // set used by the step being enqueued (-1: none)
+    int probe_idx = 0;             // next launch slot of that set
+    long long probe_step = 0;
+    unsigned long long* probe_slots = nullptr;   // [2 sets][pairs][probe_blocks][2]
+    int probe_pairs = 0;
+    long long probe_blocks = 0;                  // max blocks of one dominant-kernel launch
+    hipEvent_t probe_done[2] = {nullptr, nullptr};
+    hipStream_t probe_stream = nullptr;
+    bool probe_pending[2] = {false, false};
+    double probe_total_ms = 0.0;
+    long long probe_launches = 0;
+    double clock_check_event_us = 0.0, clock_check_stamp_us = 0.0;
     std::map<int, Graphs> graphs;  // key: train*2 + injected
 
     float* alloc(long long per_slot) {
@@ -355,7 +371,7 @@ void gemm(int layout, int epi, const GemmArgs& g, hipStream_t s) {
 void fwd_hidden(const Ctx& c, hipStream_t s, const NetLayout& N, TRef X, int ldx, int M,
                 const std::vector<float*>& U, const std::vector<float*>& G, long long act_sy,
                 const std::vector<float*>* MU, const std::vector<float*>* RS, long long st_sy,
-                bool store_u) {
+                bool store_u, bool euler = false) {
     fqlpop* h = c.h;
     for (int l = 0; l < N.L; ++l) {
         GemmArgs g{};
@@ -372,7 +388,14 @@ void fwd_hidden(const Ctx& c, hipStream_t s, const NetLayout& N, TRef X, int ldx
         g.lda = N.H; g.ldb = ldx; g.ldc = ldx;
         g.ny = N.E; g.nz = c.nz; g.slots = h->slots;
         const int epi = N.ln ? EPI_BIAS : (store_u ? EPI_BIAS_GELU2 : EPI_BIAS_GELU);
-        gemm(LAYOUT_FWD, epi, g, s);
+        if (euler && l >= 1 && epi == EPI_BIAS_GELU && g.M % 64 == 0 && g.N % 64 == 0) {
+            // the dominant kernel: its own symbol, optionally with in-kernel timing stamps
+            if (h->probe_set >= 0 && h->probe_idx < h->probe_pairs)
+                g.probe = h->probe_slots + 2 * h->probe_blocks * ((long long)h->probe_set * h->probe_pairs + h->probe_idx++);
+            launch_gemm_euler_hidden(g, s);
+        } else {
+            gemm(LAYOUT_FWD, epi, g, s);
+        }
         if (N.ln) {
             LnArgs a{};
             a.u = tref(U[l], (long long)N.H * ldx * N.E, act_sy);
@@ -495,6 +518,10 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     const int B2 = 2 * B, B3 = 3 * B;
     hipStream_t sM = h->sM, sF = h->sF, sB = h->sB, sX = h->sX;
     h->ev_next = 0;
+    h->probe_idx = 0;
+    if (h->probe_set >= 0)
+        HIPCHK(hipMemsetAsync(h->probe_slots + 2LL * h->probe_blocks * h->probe_set * h->probe_pairs, 0,
+                              sizeof(unsigned long long) * 2 * h->probe_blocks * h->probe_pairs, sM));
 
     // ---- sampling / assembly ------------------------------------------
     const auto& dset = (!train && h->ds[1].rows > 0) ? h->ds[1] : h->ds[0];
@@ -562,7 +589,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         for (int i = 1; i < S + (S == 1 ? 1 : 0); ++i) {
             // S == 1: one zero-cost pass that only clips (not used by the configs here)
             fwd_hidden(c, sF, N, tref(h->eu_in, (long long)Kb * B), B, B, h->eu_g, h->eu_g, 0,
-                       nullptr, nullptr, 0, false);
+                       nullptr, nullptr, 0, false, /*euler=*/true);
             HeadArgs he = head_args(c, N, h->eu_g[L - 1], B, B, 0);
             he.o0 = tref(h->aflow, (long long)A * B); he.ld0 = B;
             he.o2 = tref(h->eu_in, (long long)Kb * B); he.ld2 = B;
@@ -701,7 +728,8 @@ void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     }
     // one graph per (mode, active-member count): kernels read the active slot ids
     // from device memory, so any active set of the same size replays the graph
-    const int key = ((train ? 4 : 0) + (inj_batch ? 2 : 0) + (inj_noise ? 1 : 0)) + 8 * h->nz;
+    const int key = ((train ? 4 : 0) + (inj_batch ? 2 : 0) + (inj_noise ? 1 : 0)) + 8 * h->nz +
+                    (1 << 20) * (h->probe_set + 1);
     Graphs& gr = h->graphs[key];
     if (gr.exec == nullptr || gr.nz != h->nz) {
         if (gr.exec) HIPCHK(hipGraphExecDestroy(gr.exec));
@@ -720,6 +748,35 @@ void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         gr.nz = h->nz;
     }
     HIPCHK(hipGraphLaunch(gr.exec, h->sM));
+}
+
+// Launch duration from per-block stamps: max(end) - min(start) over the blocks
+// that ran (0 = slot not written).  s_memrealtime counts at 100 MHz.
+double probe_launch_us(const unsigned long long* v, long long blocks) {
+    unsigned long long lo = ~0ULL, hi = 0;
+    for (long long b = 0; b < blocks; ++b) {
+        if (v[2 * b] == 0 || v[2 * b + 1] == 0) continue;
+        lo = std::min(lo, v[2 * b]);
+        hi = std::max(hi, v[2 * b + 1]);
+    }
+    return hi > lo ? (double)(hi - lo) * 0.01 : -1.0;
+}
+
+// Accumulate the timing stamps of one probe set (waits for its step to finish).
+void probe_consume(fqlpop* h, int set) {
+    HIPCHK(hipEventSynchronize(h->probe_done[set]));
+    const long long per = 2 * h->probe_blocks;
+    std::vector<unsigned long long> v(per * h->probe_pairs);
+    HIPCHK(hipMemcpyAsync(v.data(), h->probe_slots + per * set * h->probe_pairs, sizeof(unsigned long long) * v.size(),
+                          hipMemcpyDeviceToHost, h->probe_stream));
+    HIPCHK(hipStreamSynchronize(h->probe_stream));
+    for (int p = 0; p < h->probe_pairs; ++p) {
+        const double us = probe_launch_us(v.data() + per * p, h->probe_blocks);
+        if (us < 0) continue;  // launch not probed
+        h->probe_total_ms += us * 1e-3;
+        ++h->probe_launches;
+    }
+    h->probe_pending[set] = false;
 }
 
 void update_slots(fqlpop* h) {
@@ -816,6 +873,12 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             else h->sX = h->sM;
         }
         h->ev_pool.resize(64);
+        h->probe_pairs = std::max(1, (cfg->flow_steps - 1) * (cfg->num_hidden - 1));
+        h->probe_blocks = (long long)((cfg->hidden_dim + 63) / 64) * ((cfg->batch_size + 63) / 64) * n_members;
+        HIPCHK(hipMalloc(&h->probe_slots, sizeof(unsigned long long) * 4 * h->probe_blocks * h->probe_pairs));
+        HIPCHK(hipMemset(h->probe_slots, 0, sizeof(unsigned long long) * 4 * h->probe_blocks * h->probe_pairs));
+        for (auto& e : h->probe_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(hipStreamCreateWithFlags(&h->probe_stream, hipStreamNonBlocking));
         for (auto& e : h->ev_pool) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         for (hipEvent_t* e : {&h->ev_sample, &h->ev_bcfwd, &h->ev_bcloss, &h->ev_flow, &h->ev_bdone})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -910,6 +973,10 @@ int fqlpop_destroy(fqlpop_t* h) {
         for (hipEvent_t e : {h->ev_sample, h->ev_bcfwd, h->ev_bcloss, h->ev_flow, h->ev_bdone, h->ev_t0, h->ev_t1})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+        for (hipEvent_t e : h->probe_done)
+            if (e) (void)hipEventDestroy(e);
+        if (h->probe_stream) (void)hipStreamDestroy(h->probe_stream);
+        if (h->probe_slots) (void)hipFree(h->probe_slots);
         if (h->sX && h->sX != h->sM) (void)hipStreamDestroy(h->sX);
         for (hipStream_t s : {h->sM, h->sF, h->sB})
             if (s) (void)hipStreamDestroy(s);
@@ -960,7 +1027,20 @@ int fqlpop_step(fqlpop_t* h, int n_steps) {
         ARGCHK(n_steps >= 0, "n_steps must be >= 0");
         if (h->ds[0].rows == 0) throw FqErr{FQLPOP_E_STATE, "no training dataset set (fqlpop_set_dataset)"};
         HIPCHK(hipSetDevice(h->device));
-        for (int i = 0; i < n_steps; ++i) run(h, true, false, false);
+        for (int i = 0; i < n_steps; ++i) {
+            if (h->probe) {
+                const int set = (int)(h->probe_step & 1);
+                if (h->probe_pending[set]) probe_consume(h, set);  // the step i-2 that used this set
+                h->probe_set = set;
+                run(h, true, false, false);
+                h->probe_set = -1;
+                HIPCHK(hipEventRecord(h->probe_done[set], h->sM));
+                h->probe_pending[set] = true;
+                ++h->probe_step;
+            } else {
+                run(h, true, false, false);
+            }
+        }
     });
 }
 
@@ -1214,15 +1294,55 @@ int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* 
         g.bias = pref(h, h->params, N, N.b[1]);
         g.M = H; g.N = B; g.K = H; g.lda = H; g.ldb = B; g.ldc = B;
         g.ny = 1; g.nz = h->nz; g.slots = h->slots;
-        gemm(LAYOUT_FWD, EPI_BIAS_GELU, g, h->sF);  // warm-up
+        launch_gemm_euler_hidden(g, h->sF);  // warm-up
         HIPCHK(hipEventRecord(h->ev_t0, h->sF));
-        for (int i = 0; i < iters; ++i) gemm(LAYOUT_FWD, EPI_BIAS_GELU, g, h->sF);
+        for (int i = 0; i < iters; ++i) launch_gemm_euler_hidden(g, h->sF);
         HIPCHK(hipEventRecord(h->ev_t1, h->sF));
         HIPCHK(hipEventSynchronize(h->ev_t1));
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, h->ev_t0, h->ev_t1));
         *avg_us = 1000.0 * ms / iters;
         *flops = 2.0 * H * (double)B * H * h->nz;
+        // clock cross-check of the in-kernel stamps: the same launch timed by
+        // HIP events and by its blocks' s_memrealtime stamps (slot set 0)
+        HIPCHK(hipMemsetAsync(h->probe_slots, 0, sizeof(unsigned long long) * 2 * h->probe_blocks, h->sF));
+        g.probe = h->probe_slots;
+        HIPCHK(hipEventRecord(h->ev_t0, h->sF));
+        launch_gemm_euler_hidden(g, h->sF);
+        HIPCHK(hipEventRecord(h->ev_t1, h->sF));
+        HIPCHK(hipEventSynchronize(h->ev_t1));
+        HIPCHK(hipEventElapsedTime(&ms, h->ev_t0, h->ev_t1));
+        std::vector<unsigned long long> v(2 * h->probe_blocks);
+        HIPCHK(hipMemcpy(v.data(), h->probe_slots, sizeof(unsigned long long) * v.size(), hipMemcpyDeviceToHost));
+        h->clock_check_event_us = 1000.0 * ms;
+        h->clock_check_stamp_us = probe_launch_us(v.data(), h->probe_blocks);
+    });
+}
+
+int fqlpop_set_probe(fqlpop_t* h, int enable) {
+    return guard([&] {
+        ARGCHK(h, "null handle");
+        HIPCHK(hipSetDevice(h->device));
+        for (int st = 0; st < 2; ++st)
+            if (h->probe_pending[st]) probe_consume(h, st);
+        h->probe = enable != 0;
+        h->probe_total_ms = 0.0;
+        h->probe_launches = 0;
+    });
+}
+
+int fqlpop_read_probe(fqlpop_t* h, double* total_us, int64_t* launches, double* clock_check) {
+    return guard([&] {
+        ARGCHK(h && total_us && launches, "null argument");
+        HIPCHK(hipSetDevice(h->device));
+        for (int st = 0; st < 2; ++st)
+            if (h->probe_pending[st]) probe_consume(h, st);
+        *total_us = 1000.0 * h->probe_total_ms;
+        *launches = h->probe_launches;
+        if (clock_check) {
+            clock_check[0] = h->clock_check_event_us;
+            clock_check[1] = h->clock_check_stamp_us;
+        }
     });
 }
 

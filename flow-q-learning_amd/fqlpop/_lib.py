@@ -82,6 +82,9 @@ _SIGS = {
                                                    ctypes.POINTER(ctypes.c_double),
                                                    ctypes.POINTER(ctypes.c_double)]),
     "fqlpop_flops_per_member_step": (ctypes.c_double, [ctypes.POINTER(Config)]),
+    "fqlpop_set_probe": (ctypes.c_int, [_P, ctypes.c_int]),
+    "fqlpop_read_probe": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
+                                         ctypes.POINTER(ctypes.c_double)]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
 

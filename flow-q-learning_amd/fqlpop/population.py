@@ -310,6 +310,24 @@ class Population:
         self.set_flat(member, self.tree_to_flat(sd["opt_state"]["nu"]), STATE_ADAM_V)
         self.set_count(member, int(sd["opt_state"]["count"]))
 
+    def set_probe(self, enable: bool = True):
+        check(self.lib.fqlpop_set_probe(self._h, int(bool(enable))))
+
+    def read_probe(self):
+        """(mean duration in us, launches, (event_us, stamp_us)) of the dominant
+        kernel inside step(); the pair is the last clock cross-check."""
+        tot = ctypes.c_double()
+        n = ctypes.c_int64()
+        cc = (ctypes.c_double * 2)()
+        check(self.lib.fqlpop_read_probe(self._h, ctypes.byref(tot), ctypes.byref(n), cc))
+        mean = tot.value / n.value if n.value else float("nan")
+        return mean, int(n.value), (float(cc[0]), float(cc[1]))
+
+    def dominant_kernel_flops(self) -> float:
+        """Algorithmic FLOPs of one dominant-kernel launch (all active members)."""
+        H, B = self.cfg.hidden_dims[0], self.cfg.batch_size
+        return 2.0 * H * H * B * int(self.active.sum())
+
     def time_dominant_kernel(self, iters: int = 50):
         us = ctypes.c_double()
         fl = ctypes.c_double()

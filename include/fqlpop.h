@@ -166,6 +166,16 @@ int fqlpop_sync(fqlpop_t* h);
  * duration (us) and the algorithmic FLOPs of one launch. */
 int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* flops);
 
+/* In-step timing probe of the dominant kernel (bench.py's roofline): while
+ * enabled, every Euler-flow hidden-layer GEMM launch inside fqlpop_step
+ * stamps the 100 MHz s_memrealtime clock at the start and end of each of its
+ * blocks; a launch lasts max(end) - min(start).  read_probe returns the total
+ * (us) and number of launches timed since set_probe (which resets them), and
+ * if clock_check != NULL the last fqlpop_time_dominant_kernel cross-check:
+ * [0] one isolated launch timed by HIP events, [1] the same by its stamps. */
+int fqlpop_set_probe(fqlpop_t* h, int enable);
+int fqlpop_read_probe(fqlpop_t* h, double* total_us, int64_t* launches, double* clock_check);
+
 /* Algorithmic GEMM FLOPs of one member-update at the handle's config
  * (SURVEY.md 8d formula). */
 double fqlpop_flops_per_member_step(const fqlpop_config* cfg);
