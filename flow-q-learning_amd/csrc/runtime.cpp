@@ -843,6 +843,8 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         ARGCHK(cfg->batch_size >= 64 && cfg->batch_size % 64 == 0, "batch_size must be a multiple of 64");
         ARGCHK(cfg->num_qs >= 1 && cfg->num_qs <= 4, "num_qs must be in [1, 4]");
         ARGCHK(cfg->flow_steps >= 2, "flow_steps must be >= 2");
+        if (cfg->actor_layer_norm)
+            throw FqErr{FQLPOP_E_UNSUPPORTED, "actor_layer_norm is not supported yet (reference default False)"};
         auto h = std::make_unique<fqlpop>();
         h->cfg = *cfg;
         h->n = n_members;
@@ -866,7 +868,7 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         HIPCHK(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
         // A 4th stream (target critic + dW GEMMs + Adams off the main chain) is
         // opt-in: on MI355X the step is throughput-bound and the extra
-        // concurrency measured 5% slower (profiles/round1_notes.md).
+        // concurrency measured 5% slower.
         {
             const char* ns = std::getenv("FQLPOP_STREAMS");
             if (ns && std::atoi(ns) >= 4) HIPCHK(hipStreamCreateWithFlags(&h->sX, hipStreamNonBlocking));

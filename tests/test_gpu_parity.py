@@ -103,6 +103,46 @@ def test_update_parity_q_min_normalized():
     _run_parity(64, 64, [30.0], n_steps=2, q_agg="min", normalize_q_loss=True)
 
 
+@pytest.mark.parametrize("H,B,kw", [
+    (128, 64, dict(layer_norm=False)),            # critic without LayerNorm
+    (256, 128, dict(flow_steps=3, discount=0.995)),  # antsoccer reproduce discount
+    (1024, 64, dict()),                           # widest supported hidden dim
+    (64, 192, dict(q_agg="min", tau=0.05)),       # odd multiple of 64 rows
+])
+def test_update_parity_configs(H, B, kw):
+    _run_parity(H, B, [4.0, 40.0], n_steps=2, **kw)
+
+
+def test_update_parity_ant_full_size():
+    """BASELINE config C3 shapes: obs 42, act 8, H=512, B=1024 (one step)."""
+    from fqlpop import Population, PopulationConfig
+    H, B = 512, 1024
+    ocfg = O.OracleConfig(obs_dim=42, action_dim=8, hidden_dims=(H,) * 4, batch_size=B, alpha=10.0,
+                          discount=0.995)
+    pop = Population(PopulationConfig(obs_dim=42, action_dim=8, hidden_dims=(H,) * 4, batch_size=B,
+                                      discount=0.995), [10.0], [3])
+    p = _f32(O.init_params(ocfg, 21))
+    o = O.init_opt_state(p)
+    pop.set_params(0, O.cast_tree(p, np.float32))
+    rng = np.random.default_rng(77)
+    b = O.cast_tree(O.make_batch(ocfg, B, rng), np.float32)
+    n = O.cast_tree(O.make_noise(ocfg, B, rng), np.float32)
+    pop.step_injected([b], [n])
+    p, o, oinfo = O.update(ocfg, p, o, O.cast_tree(b, np.float64), O.cast_tree(n, np.float64))
+    _check_info(pop.read_info()[0], oinfo, O.TRAIN_INFO_KEYS, "ant full")
+    _check_params(pop.get_params(0), p, ocfg.lr, "ant full")
+
+
+def test_unsupported_configs_fail_loudly():
+    from fqlpop import Population, PopulationConfig
+    from fqlpop._lib import FqlpopError
+    for kw in (dict(actor_layer_norm=True), dict(hidden_dims=(96,) * 4), dict(batch_size=100)):
+        base = dict(hidden_dims=(64,) * 4, batch_size=64)
+        base.update(kw)
+        with pytest.raises(FqlpopError):
+            Population(PopulationConfig(**base), [1.0], [0])
+
+
 def test_update_parity_ant_shape():
     """antsoccer shapes (obs 42, act 8) at reduced width, B=128."""
     from fqlpop import Population, PopulationConfig

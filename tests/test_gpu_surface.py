@@ -143,3 +143,28 @@ def test_tune_alpha_driver(tmp_path):
     tune_alpha.main(common + ["--number_of_alphas=3", "--number_of_seeds=2", "--single_experiment", "--job_id=4"])
     ckpts = list((tmp_path / "cube-single-play-singletask-task2-v0").glob("*/checkpoint_20.pkl"))
     assert len(ckpts) >= 1
+
+
+def test_integration_md_binding_stub():
+    """The reference-side ctypes stub printed in INTEGRATION.md section 3 runs
+    against the built library and agrees with the shipped surface."""
+    import fqlpop._lib as L
+    from trainer.config import AgentConfig
+    from dataclasses import asdict
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    text = open(os.path.join(root, "INTEGRATION.md")).read()
+    code = text.split("```python", 1)[1].split("```", 1)[0]
+    code = code.replace('ctypes.CDLL("libfqlpop.so")', f'ctypes.CDLL({L.LIB_PATH!r})')
+    ns = {}
+    exec(compile(code, "INTEGRATION.md", "exec"), ns)
+    cfg = asdict(AgentConfig(actor_hidden_dims=(64,) * 4, value_hidden_dims=(64,) * 4, batch_size=64))
+    rng = np.random.default_rng(3)
+    ocfg = O.OracleConfig(hidden_dims=(64,) * 4, batch_size=64)
+    batch = O.cast_tree(O.make_batch(ocfg, 64, rng), np.float32)
+    agent = ns["FQLAgent"].create(5, batch["observations"][:1], batch["actions"][:1], cfg)
+    agent, info = agent.update(batch)
+    assert set(info) == set(O.TRAIN_INFO_KEYS) and all(np.isfinite(v) for v in info.values())
+    loss, vinfo = agent.total_loss(batch)
+    assert np.isfinite(loss) and len(vinfo) == 10
+    acts = agent.sample_actions(batch["observations"][:9], seed=np.array([0, 1], np.uint32))
+    assert acts.shape == (9, 5) and np.all(np.abs(acts) <= 1)
