@@ -176,20 +176,18 @@ def main():
     value = member_steps / el
     flops_ms = pop.flops_per_member_step
 
-    # dominant kernel: Euler-flow hidden-layer forward GEMM (all members, one launch)
-    kflops = pop.dominant_kernel_flops()
+    # dominant kernel of the step (all members, one launch): the persistent
+    # Euler flow (H = 512) or else the Euler hidden-layer GEMM
+    kname, kflops, kbytes = pop.dominant_kernel_info()
     iso_us, _ = pop.time_dominant_kernel(args.kernel_iters)  # the same launch replayed alone
     _, _, (cc_event_us, cc_stamp_us) = pop.read_probe()     # stamp clock vs HIP events, one launch
     launch_us = probe_us if probe_n else iso_us
     achieved = kflops / (launch_us * 1e-6) / 1e12
-    # algorithmic bytes of one launch: W (H x H) + x' (H x B) + bias read, y' (H x B) written, per member
-    H, B = pcfg.hidden_dims[0], pcfg.batch_size
-    kbytes = 4.0 * (H * H + H * B + H + H * B) * pop.n
     traffic = None
     if os.path.exists(args.pmc_json):
         with open(args.pmc_json) as f:
             pmc = json.load(f)
-        if pmc.get("kernel_regex") and pmc.get("members") == pop.n:
+        if pmc.get("kernel_regex") == kname and pmc.get("members") == pop.n:
             traffic = pmc["traffic_bytes_per_launch"]
 
     result = {
@@ -221,8 +219,9 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "gemm_fwd_dma_kernel<64, 64, 4, 3, 1> (Euler-flow hidden layer: y' = gelu(W^T x' + b), "
-                      "512x512 @ 512x256 per member, 16 members per launch)",
+            "kernel": kname + (" (Euler flow steps 1..9 of all members: 16-column blocks, weights streamed, "
+                               "activations LDS-resident)" if kname == "euler_flow_kernel" else
+                               " (Euler-flow hidden layer y' = gelu(W^T x' + b), one launch per layer)"),
             "achieved": round(achieved, 3),
             "peak": MI355X_FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",

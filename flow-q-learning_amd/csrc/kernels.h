@@ -49,6 +49,29 @@ void launch_gemm_euler_hidden(const GemmArgs& a, hipStream_t s);
 // variant: bit 0 = K slice 64 (else 32), bit 1 = two accumulator chains
 void launch_gemm_variant(int layout, int epi, int tile, int variant, const GemmArgs& a, hipStream_t s);
 
+// --------------------------------------------------- persistent Euler flow --
+// Euler steps first..S-1 of the BC flow (compute_flow_actions) for every active
+// member in ONE launch.  A block owns 16 minibatch columns of one member for
+// the whole chain: the activation slab x'[H][16] stays in LDS across layers
+// and steps, the weights stream from L2 into MFMA fragments.  H = 512 only
+// (euler_flow_supported); the caller falls back to per-layer launches.
+constexpr int EF_MAX_LAYERS = 8;
+struct EulerArgs {
+    const float* params;                  // params arena (slot stride P)
+    long long P;
+    long long w_off[EF_MAX_LAYERS + 1];   // Dense_l kernel offset inside a slot (l = 0..L, L = head)
+    long long b_off[EF_MAX_LAYERS + 1];   // Dense_l bias offset
+    TRef eu;                              // [D+A+1][B] state after step first-1 (s rows, x rows)
+    TRef aflow;                           // out [A][B]: clip(x) after the last step
+    int D, A, H, L, B, S, first;
+    float steps_f;
+    int nz;
+    const int* slots;
+    unsigned long long* probe;            // optional per-block {start, end} stamps
+};
+bool euler_flow_supported(int H, int L, int D, int A, int B);
+void launch_euler_flow(const EulerArgs& a, hipStream_t s);
+
 // ------------------------------------------------------- row-wise kernels --
 struct LnArgs {           // h = LN(gelu(u)) * gamma + beta, per column
     TRef u, h, mu, rstd, gamma, beta;

@@ -18,6 +18,7 @@
 namespace fq {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define DEV __device__ __forceinline__
 
@@ -510,6 +511,161 @@ void launch_gemm(int layout, int epi, int tile, const GemmArgs& a, hipStream_t s
 void launch_gemm_euler_hidden(const GemmArgs& a, hipStream_t s) {
     const dim3 grid((a.M / 64) * (a.N / 64) * a.ny * a.nz);
     hipLaunchKernelGGL((gemm_fwd_dma_kernel<64, 64, 4, EPI_BIAS_GELU, 1>), grid, dim3(256), 0, s, a);
+}
+
+// ==================================================== persistent Euler flow ==
+// compute_flow_actions ([EXT] fql/agents/fql.py; SURVEY.md App. A "Flow
+// target"): x <- x + v_theta(s, x, i/S) / S for i = first..S-1, then clip.
+// One block = 16 minibatch columns of one member for the WHOLE chain, so the
+// activation slab x'[512][16] never leaves LDS and there is one launch per
+// population step instead of 5 per Euler step.  8 waves split the 512 output
+// features (64 each).  The weights stream from L2 straight into MFMA A
+// fragments (v_mfma_f32_16x16x4_f32): lane (li = l&15, lk = l>>4) loads the
+// float4 W[4s+lk][64w+4li .. +3], whose component c feeds accumulator tile c,
+// so tile c row li is feature 64w + 4li + c (a fixed permutation the epilogue
+// undoes).  An 8-deep register ring of W loads runs across layer boundaries
+// (the refill of a layer's last 8 k-steps fetches the next layer's first 8);
+// the B fragment (x'[4s+lk][li], LDS) is read one k-step ahead.
+// Layer 0 input [s; x; t] is K0 = D+A+1 rows, zero-padded to a multiple of 32
+// (the padded rows multiply finite parameter words by exact zeros).
+constexpr int EF_H = 512, EF_NC = 16, EF_NW = 8, EF_PF = 8, EF_K0MAX = 64;
+
+// tanh(y) = 1 - 2 / (1 + e^{2y}) on v_exp_f32 (no libm branches)
+DEV float gelu_fast(float x) {
+    const float y = kSqrt2OverPi * (x + 0.044715f * x * x * x);
+    const float t = 1.0f - 2.0f / (1.0f + __expf(2.0f * y));
+    return 0.5f * x * (1.0f + t);
+}
+
+bool euler_flow_supported(int H, int L, int D, int A, int B) {
+    return H == EF_H && L >= 1 && L <= EF_MAX_LAYERS && D + A + 1 <= EF_K0MAX && A <= 8 && B % EF_NC == 0;
+}
+
+__global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerArgs g) {
+    constexpr int H = EF_H, NC = EF_NC, NT = EF_NW * 64, PF = EF_PF;
+    // LDS kept to ~69 KB so that blocks of the kernels running concurrently on
+    // the other streams still fit beside this one on a CU (biases and the head
+    // weights live in registers; the head reduction reuses the idle slab)
+    __shared__ __attribute__((aligned(16))) float slab[2][H * NC];
+    __shared__ __attribute__((aligned(16))) float in0[EF_K0MAX * NC + 64];  // + slack for the look-ahead read
+    __shared__ float b5s[8];
+
+    const int tiles = g.B / NC;
+    const int total = tiles * g.nz;
+    const int bid = xcd_remap(blockIdx.x, total);
+    const int z = bid / tiles, c0 = (bid % tiles) * NC;
+    const int slot = g.slots[z];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    if (g.probe != nullptr && tid == 0) g.probe[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+
+    const int D = g.D, A = g.A, L = g.L, B = g.B, S = g.S;
+    const int K0 = D + A + 1, NS0 = (K0 + 4 * PF - 1) / (4 * PF) * PF;  // padded k-steps of layer 0
+    const float* __restrict__ P = g.params + (long long)slot * g.P;
+    const float* __restrict__ eu = at(g.eu, slot);
+    for (int e = tid; e < EF_K0MAX * NC + 64; e += NT) {
+        const int r = e / NC, j = e % NC;
+        in0[e] = (r < D + A) ? eu[(long long)r * B + c0 + j] : 0.f;
+    }
+    if (tid < A) b5s[tid] = P[g.b_off[L] + tid];
+    // head A fragments (constant over the flow): W_L[64w + 4s + lk][li], li < A
+    float w5r[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) w5r[s] = li < A ? P[g.w_off[L] + (64 * w + 4 * s + lk) * A + li] : 0.f;
+
+    const rsrc_t rW = make_rsrc(P, g.P);
+    const int lo = lk * H + 64 * w + 4 * li;
+    float4 ring[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) ring[p] = bload4(rW, (int)g.w_off[0] + 4 * p * H + lo);
+    __syncthreads();
+
+    for (int step = g.first; step < S; ++step) {
+        if (tid < NC) in0[(D + A) * NC + tid] = (float)((double)step / (double)S);
+        __syncthreads();
+        for (int l = 0; l < L; ++l) {
+            const int NS = l == 0 ? NS0 : H / 4;
+            const float* xs = l == 0 ? in0 : slab[(l - 1) & 1];
+            float* xo = slab[l & 1];
+            const int nl = l + 1 < L ? l + 1 : 0;
+            f32x4 acc[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+            // this lane's 16 bias values (features 64w + 16lk + 4r + c), in flight during the k-loop
+            float4 bias4[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bias4[r] = bload4(rW, (int)g.b_off[l] + 64 * w + 16 * lk + 4 * r);
+            float bnext = xs[lk * NC + li];
+            for (int s0 = 0; s0 < NS; s0 += PF) {
+                // refill targets: k-steps s0+PF.. of this layer, or the next layer's first PF
+                const int rbase = (s0 + PF < NS ? (int)g.w_off[l] + 4 * (s0 + PF) * H : (int)g.w_off[nl]) + lo;
+#pragma unroll
+                for (int p = 0; p < PF; ++p) {
+                    const int s = s0 + p;
+                    const float b = bnext;
+                    bnext = xs[(4 * (s + 1) + lk) * NC + li];  // one k-step ahead (past the end: unused)
+                    __builtin_amdgcn_sched_barrier(0);
+                    const float4 a = ring[p];
+                    acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b, acc[0], 0, 0, 0);
+                    acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b, acc[1], 0, 0, 0);
+                    acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b, acc[2], 0, 0, 0);
+                    acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b, acc[3], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    ring[p] = bload4(rW, rbase + 4 * p * H);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            // tile c, reg r, lane (lk, li): feature 64w + 4(4lk + r) + c, column li
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float bb[4] = {bias4[r].x, bias4[r].y, bias4[r].z, bias4[r].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int f = 64 * w + 4 * (4 * lk + r) + c;
+                    xo[f * NC + li] = gelu_fast(acc[c][r] + bb[c]);
+                }
+            }
+            __syncthreads();
+        }
+        // head: v[a][j] = sum_k W_L[k][a] h[k][j] + b_L[a]; wave w sums k in [64w, 64w+64)
+        float* red = slab[L & 1];  // [EF_NW][16 x NC] partial head tiles (this slab is idle now)
+        {
+            const float* hs = slab[(L - 1) & 1];
+            f32x4 hacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                const int k = 64 * w + 4 * s + lk;
+                hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(w5r[s], hs[k * NC + li], hacc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[w * 16 * NC + (4 * lk + r) * NC + li] = hacc[r];
+        }
+        __syncthreads();
+        if (tid < A * NC) {
+            const int a = tid / NC, j = tid % NC;
+            float v = red[tid];
+#pragma unroll
+            for (int q = 1; q < EF_NW; ++q) v += red[q * 16 * NC + tid];
+            v += b5s[a];
+            float* xp = &in0[(D + a) * NC + j];
+            *xp = *xp + v / g.steps_f;
+        }
+        __syncthreads();
+    }
+    if (tid < A * NC) {
+        const int a = tid / NC, j = tid % NC;
+        at(g.aflow, slot)[(long long)a * B + c0 + j] = clip1(in0[(D + a) * NC + j]);
+    }
+    if (g.probe != nullptr) {
+        __syncthreads();
+        if (tid == 0) g.probe[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+void launch_euler_flow(const EulerArgs& a, hipStream_t s) {
+    const dim3 grid((a.B / EF_NC) * a.nz);
+    hipLaunchKernelGGL(euler_flow_kernel, grid, dim3(EF_NW * 64), 0, s, a);
 }
 
 // ================================================= column-reduction kernels ==

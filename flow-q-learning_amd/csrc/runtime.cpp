@@ -165,6 +165,7 @@ struct fqlpop {
     // in-step timing probe of the dominant kernel (Euler hidden-layer GEMM):
     // its blocks stamp s_memrealtime into per-launch slots; two slot sets are
     // used by alternate steps so the host reads step i-2 while step i runs
+    bool euler_fused = false;      // Euler steps 1..S-1 as one persistent launch (euler_flow_kernel)
     bool probe = false;
     int probe_set = -1;            // set used by the step being enqueued (-1: none)
     int probe_idx = 0;             // next launch slot of that set
@@ -510,6 +511,33 @@ void adam_net(const Ctx& c, hipStream_t s, int ni) {
     launch_adam(a, s);
 }
 
+// Arguments of the persistent Euler-flow launch: steps 1..S-1 from eu_in (the
+// state the BC head left after step 0) to aflow.
+EulerArgs euler_args(fqlpop* h, int nz) {
+    const NetLayout& N = h->bc;
+    EulerArgs ea{};
+    ea.params = h->params + N.off;
+    ea.P = h->P;
+    for (int l = 0; l <= N.L; ++l) {
+        ea.w_off[l] = N.W[l];
+        ea.b_off[l] = N.b[l];
+    }
+    ea.eu = tref(h->eu_in, (long long)(h->D + h->A + 1) * h->B);
+    ea.aflow = tref(h->aflow, (long long)h->A * h->B);
+    ea.D = h->D; ea.A = h->A; ea.H = h->H; ea.L = h->L; ea.B = h->B; ea.S = h->S; ea.first = 1;
+    ea.steps_f = (float)h->S;
+    ea.nz = nz; ea.slots = h->slots;
+    return ea;
+}
+
+// Algorithmic FLOPs of one dominant launch over the active members.
+double dominant_flops(const fqlpop* h) {
+    const double B = h->B, H = h->H, K0 = h->D + h->A + 1, A = h->A;
+    if (h->euler_fused)
+        return (h->S - 1) * 2.0 * B * (K0 * H + (h->L - 1) * H * H + H * A) * h->nz;
+    return 2.0 * H * B * H * h->nz;
+}
+
 // Enqueue one population update (train) or one total_loss pass (!train).
 void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     const Ctx c{h, h->nz};
@@ -586,7 +614,13 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         ha.t_next = (float)(1.0 / (double)S);
         launch_head_fwd(HEAD_BC_FUSED, ha, sF);
         HIPCHK(hipEventRecord(h->ev_bcfwd, sF));
-        for (int i = 1; i < S + (S == 1 ? 1 : 0); ++i) {
+        if (h->euler_fused) {
+            EulerArgs ea = euler_args(h, c.nz);
+            if (h->probe_set >= 0 && h->probe_idx < h->probe_pairs)
+                ea.probe = h->probe_slots + 2 * h->probe_blocks * ((long long)h->probe_set * h->probe_pairs + h->probe_idx++);
+            launch_euler_flow(ea, sF);
+        }
+        for (int i = 1; !h->euler_fused && i < S + (S == 1 ? 1 : 0); ++i) {
             // S == 1: one zero-cost pass that only clips (not used by the configs here)
             fwd_hidden(c, sF, N, tref(h->eu_in, (long long)Kb * B), B, B, h->eu_g, h->eu_g, 0,
                        nullptr, nullptr, 0, false, /*euler=*/true);
@@ -875,8 +909,17 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             else h->sX = h->sM;
         }
         h->ev_pool.resize(64);
-        h->probe_pairs = std::max(1, (cfg->flow_steps - 1) * (cfg->num_hidden - 1));
-        h->probe_blocks = (long long)((cfg->hidden_dim + 63) / 64) * ((cfg->batch_size + 63) / 64) * n_members;
+        {
+            const char* ef = std::getenv("FQLPOP_EULER");
+            h->euler_fused = euler_flow_supported(H, L, D, A, B) && !h->bc.ln && !(ef && std::atoi(ef) == 0);
+        }
+        if (h->euler_fused) {  // dominant kernel: one persistent Euler launch per step
+            h->probe_pairs = 1;
+            h->probe_blocks = (long long)(cfg->batch_size / 16) * n_members;
+        } else {               // dominant kernel: the Euler hidden-layer GEMMs
+            h->probe_pairs = std::max(1, (cfg->flow_steps - 1) * (cfg->num_hidden - 1));
+            h->probe_blocks = (long long)((cfg->hidden_dim + 63) / 64) * ((cfg->batch_size + 63) / 64) * n_members;
+        }
         HIPCHK(hipMalloc(&h->probe_slots, sizeof(unsigned long long) * 4 * h->probe_blocks * h->probe_pairs));
         HIPCHK(hipMemset(h->probe_slots, 0, sizeof(unsigned long long) * 4 * h->probe_blocks * h->probe_pairs));
         for (auto& e : h->probe_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1288,7 +1331,10 @@ int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* 
         HIPCHK(hipDeviceSynchronize());
         const NetLayout& N = h->bc;
         const int B = h->B, H = h->H;
-        // Euler hidden layer 1: eu_g[1] = gelu(W1^T eu_g[0] + b1), all active members
+        // the dominant launch, replayed alone on sF with the buffers of the last step:
+        // the persistent Euler flow (reads eu_in, writes aflow: idempotent), or
+        // Euler hidden layer 1: eu_g[1] = gelu(W1^T eu_g[0] + b1)
+        EulerArgs ea = euler_args(h, h->nz);
         GemmArgs g{};
         g.A = pref(h, h->params, N, N.W[1]);
         g.B = tref(h->eu_g[0], (long long)H * B);
@@ -1296,21 +1342,29 @@ int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* 
         g.bias = pref(h, h->params, N, N.b[1]);
         g.M = H; g.N = B; g.K = H; g.lda = H; g.ldb = B; g.ldc = B;
         g.ny = 1; g.nz = h->nz; g.slots = h->slots;
-        launch_gemm_euler_hidden(g, h->sF);  // warm-up
+        auto launch = [&](unsigned long long* probe) {
+            if (h->euler_fused) {
+                ea.probe = probe;
+                launch_euler_flow(ea, h->sF);
+            } else {
+                g.probe = probe;
+                launch_gemm_euler_hidden(g, h->sF);
+            }
+        };
+        launch(nullptr);  // warm-up
         HIPCHK(hipEventRecord(h->ev_t0, h->sF));
-        for (int i = 0; i < iters; ++i) launch_gemm_euler_hidden(g, h->sF);
+        for (int i = 0; i < iters; ++i) launch(nullptr);
         HIPCHK(hipEventRecord(h->ev_t1, h->sF));
         HIPCHK(hipEventSynchronize(h->ev_t1));
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, h->ev_t0, h->ev_t1));
         *avg_us = 1000.0 * ms / iters;
-        *flops = 2.0 * H * (double)B * H * h->nz;
+        *flops = dominant_flops(h);
         // clock cross-check of the in-kernel stamps: the same launch timed by
         // HIP events and by its blocks' s_memrealtime stamps (slot set 0)
         HIPCHK(hipMemsetAsync(h->probe_slots, 0, sizeof(unsigned long long) * 2 * h->probe_blocks, h->sF));
-        g.probe = h->probe_slots;
         HIPCHK(hipEventRecord(h->ev_t0, h->sF));
-        launch_gemm_euler_hidden(g, h->sF);
+        launch(h->probe_slots);
         HIPCHK(hipEventRecord(h->ev_t1, h->sF));
         HIPCHK(hipEventSynchronize(h->ev_t1));
         HIPCHK(hipEventElapsedTime(&ms, h->ev_t0, h->ev_t1));
@@ -1318,6 +1372,24 @@ int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* 
         HIPCHK(hipMemcpy(v.data(), h->probe_slots, sizeof(unsigned long long) * v.size(), hipMemcpyDeviceToHost));
         h->clock_check_event_us = 1000.0 * ms;
         h->clock_check_stamp_us = probe_launch_us(v.data(), h->probe_blocks);
+    });
+}
+
+int fqlpop_dominant_kernel_info(fqlpop_t* h, char* name, int name_cap, double* flops, double* bytes) {
+    return guard([&] {
+        ARGCHK(h && name && name_cap > 0 && flops && bytes, "null argument");
+        const double B = h->B, H = h->H, K0 = h->D + h->A + 1, A = h->A, L = h->L, nz = h->nz;
+        std::string nm;
+        if (h->euler_fused) {
+            nm = "euler_flow_kernel";
+            // unique bytes: the bc net's Dense kernels + biases, the state in, a_flow out
+            *bytes = 4.0 * nz * (K0 * H + (L - 1) * H * H + H * A + L * H + A + K0 * B + A * B);
+        } else {
+            nm = "gemm_fwd_dma_kernel<64, 64, 4, 3, 1>";
+            *bytes = 4.0 * nz * (H * H + H * B + H + H * B);
+        }
+        *flops = dominant_flops(h);
+        std::snprintf(name, name_cap, "%s", nm.c_str());
     });
 }
 

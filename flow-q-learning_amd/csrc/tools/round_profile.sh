@@ -7,7 +7,7 @@ set -euo pipefail
 TAG=${1:-r}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
-K='gemm_fwd_dma_kernel<64, 64, 4, 3, 1>'
+K=${2:-euler_flow_kernel}   # dominant kernel symbol (fqlpop_dominant_kernel_info)
 timeout -k 10 400 python "$R/bench.py" > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err"
 timeout -k 10 300 python "$R/bench.py" --no-probe --no-cpu-baseline > "$O/bench_${TAG}_noprobe.json" 2>> "$O/bench_$TAG.err"
 cd /tmp && export TMPDIR=/tmp

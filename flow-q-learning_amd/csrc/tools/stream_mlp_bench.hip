@@ -1,0 +1,209 @@
+// Developer micro-benchmark: a "column-resident, weight-streamed" MLP chain.
+// A block owns NC=16 columns of one member for ALL H=512 features, keeps the
+// activation slab x'[H][16] in LDS across layers and streams the weights
+// W[k][i] straight from global memory into MFMA A fragments (16x16x4 f32),
+// with a PF-deep register prefetch ring.  Measures TFLOP/s of 3 chained
+// 512x512 hidden layers (gelu epilogue) for 16 members x 256 columns, and
+// checks against a naive GPU reference.
+//   ./stream_mlp_bench [members=16] [iters=20]
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                                       \
+    do {                                                                                            \
+        hipError_t e = (x);                                                                         \
+        if (e != hipSuccess) {                                                                      \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            std::exit(1);                                                                           \
+        }                                                                                           \
+    } while (0)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, long long n_elems) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(n_elems * 4), 0x00020000);
+}
+__device__ __forceinline__ float4 bload4(rsrc_t r, int elem_off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, elem_off * 4, 0, 0));
+}
+constexpr int H = 512, NC = 16, LAYERS = 3;
+
+__device__ __forceinline__ float gelu_f(float x) {
+    const float y = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.0f + tanhf(y));
+}
+// tanh(y) = 1 - 2 / (1 + e^{2y}) on v_exp_f32 (no libm branches)
+__device__ __forceinline__ float gelu_fast(float x) {
+    const float y = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+    const float t = 1.0f - 2.0f / (1.0f + __expf(2.0f * y));
+    return 0.5f * x * (1.0f + t);
+}
+
+// W: [member][layer][k=H][i=H] ; bias [member][layer][H] ; X: [member][H][ncols] (feature-major)
+// NW waves split the H output features (FW = H/NW each, TQ = FW/64 float4 W loads
+// per lane per k-step); the W ring runs across layer boundaries (the refill of
+// the last PF k-steps of layer l fetches the first ones of layer l+1).
+template <int PF, int NW, bool ROT>
+__global__ __launch_bounds__(64 * NW, 1) void mlp_stream16(const float* __restrict__ W, const float* __restrict__ bias,
+                                                           const float* __restrict__ X, float* __restrict__ Y,
+                                                           int ncols) {
+    constexpr int NT = 64 * NW, FW = H / NW, TQ = FW / 64, NTL = 4 * TQ;
+    __shared__ __attribute__((aligned(16))) float slab[2][H * NC];
+    __shared__ float bs[LAYERS][H];
+    const int tiles = ncols / NC;
+    // XCD-aware: the 8 XCDs take blocks round-robin; give each XCD a contiguous
+    // range of logical blocks so one member's column tiles share an L2
+    const int total = gridDim.x, q = total >> 3, rr = total & 7, x = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int bid = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + loc;
+    const int m = bid / tiles, c0 = (bid % tiles) * NC;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    for (int e = tid; e < H * NC; e += NT) {
+        const int f = e / NC, j = e % NC;
+        slab[0][e] = X[((long long)m * H + f) * ncols + c0 + j];
+    }
+    for (int e = tid; e < LAYERS * H; e += NT) bs[e / H][e % H] = bias[(long long)m * LAYERS * H + e];
+    const rsrc_t rW = make_rsrc(W + (long long)m * LAYERS * H * H, (long long)LAYERS * H * H);
+    const int lo = lk * H + FW * w + 4 * li;  // + 4 s H (+ 64 q)
+    constexpr int NS = H / 4;                 // k-steps per layer
+    // ROT: each column tile walks K from its own starting step, so the 16 tiles
+    // of a member do not hammer the same L2 channels in lockstep
+    const int s_rot = ROT ? ((bid % tiles) * (NS / tiles)) & (NS - 1) : 0;
+    float4 ring[PF][TQ];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+#pragma unroll
+        for (int t = 0; t < TQ; ++t) ring[p][t] = bload4(rW, lo + 4 * ((s_rot + p) & (NS - 1)) * H + 64 * t);
+    __syncthreads();
+    int cur = 0;
+    for (int l = 0; l < LAYERS; ++l) {
+        f32x4 acc[NTL];
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* xs = slab[cur];
+        const int lbase = lo + l * H * H;
+        float bnext = xs[(4 * s_rot + lk) * NC + li];
+        for (int s0 = 0; s0 < NS; s0 += PF) {
+#pragma unroll
+            for (int p = 0; p < PF; ++p) {
+                const int s = s0 + p;
+                const float b = bnext;
+                bnext = xs[(4 * ((s_rot + s + 1) & (NS - 1)) + lk) * NC + li];  // one step ahead
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int t = 0; t < TQ; ++t) {
+                    const float4 a = ring[p][t];
+                    acc[4 * t + 0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b, acc[4 * t + 0], 0, 0, 0);
+                    acc[4 * t + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b, acc[4 * t + 1], 0, 0, 0);
+                    acc[4 * t + 2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b, acc[4 * t + 2], 0, 0, 0);
+                    acc[4 * t + 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b, acc[4 * t + 3], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                {
+                    const int j = s + PF;  // ring refill: k-step j of this layer or j - NS of the next
+                    const int off = lbase + (j >= NS ? H * H : 0) + 4 * ((s_rot + j) & (NS - 1)) * H;
+#pragma unroll
+                    for (int t = 0; t < TQ; ++t) ring[p][t] = bload4(rW, off + 64 * t);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // epilogue: tile 4t + c, reg r, lane (lk, li): feature FW w + 64 t + 4 (4 lk + r) + c, column li
+        float* xo = slab[cur ^ 1];
+#pragma unroll
+        for (int tt = 0; tt < NTL; ++tt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int f = FW * w + 64 * (tt >> 2) + 4 * (4 * lk + r) + (tt & 3);
+                xo[f * NC + li] = gelu_fast(acc[tt][r] + bs[l][f]);
+            }
+        __syncthreads();
+        cur ^= 1;
+    }
+    for (int e = tid; e < H * NC; e += NT) {
+        const int f = e / NC, j = e % NC;
+        Y[((long long)m * H + f) * ncols + c0 + j] = slab[cur][e];
+    }
+}
+
+__global__ void ref_layer(const float* W, const float* bias, const float* X, float* Y, int ncols, int l) {
+    const int m = blockIdx.z, i = blockIdx.y, j = blockIdx.x * 64 + threadIdx.x;
+    if (j >= ncols) return;
+    const float* Wl = W + ((long long)m * LAYERS + l) * H * H;
+    float s = 0.f;
+    for (int k = 0; k < H; ++k) s = fmaf(Wl[(long long)k * H + i], X[((long long)m * H + k) * ncols + j], s);
+    Y[((long long)m * H + i) * ncols + j] = gelu_f(s + bias[((long long)m * LAYERS + l) * H + i]);
+}
+
+__global__ void fill(float* p, long long n, unsigned seed, float scale) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    unsigned x = (unsigned)i * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    p[i] = ((x & 0xFFFFFF) / 16777216.0f - 0.5f) * scale;
+}
+
+template <int PF, int NW, bool ROT>
+void run(int nm, int iters, const float* W, const float* b, const float* X, float* Y, const std::vector<float>& ref,
+         int ncols, hipStream_t s) {
+    const dim3 grid(nm * (ncols / NC));
+    hipLaunchKernelGGL((mlp_stream16<PF, NW, ROT>), grid, dim3(64 * NW), 0, s, W, b, X, Y, ncols);
+    CK(hipStreamSynchronize(s));
+    std::vector<float> got(ref.size());
+    CK(hipMemcpy(got.data(), Y, sizeof(float) * got.size(), hipMemcpyDeviceToHost));
+    double err = 0;
+    for (size_t i = 0; i < got.size(); ++i) err = std::max(err, (double)std::fabs(got[i] - ref[i]));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((mlp_stream16<PF, NW, ROT>), grid, dim3(64 * NW), 0, s, W, b, X, Y, ncols);
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1000.0 * ms / iters;
+    const double fl = 2.0 * H * H * (double)ncols * nm * LAYERS;
+    std::printf("stream16 ROT=%d NW=%d PF=%d  members %d cols %d: %8.2f us per 3 layers  %7.2f TFLOP/s  maxerr %.2e\n", (int)ROT, NW, PF, nm,
+                ncols, us, fl / us / 1e6, err);
+}
+
+int main(int argc, char** argv) {
+    const int nm = argc > 1 ? std::atoi(argv[1]) : 16;
+    const int iters = argc > 2 ? std::atoi(argv[2]) : 20;
+    const int ncols = 256;
+    const long long nW = (long long)nm * LAYERS * H * H, nb = (long long)nm * LAYERS * H,
+                    nX = (long long)nm * H * ncols;
+    float *W, *b, *X, *Y, *T0, *T1;
+    CK(hipMalloc(&W, 4 * nW));
+    CK(hipMalloc(&b, 4 * nb));
+    CK(hipMalloc(&X, 4 * nX));
+    CK(hipMalloc(&Y, 4 * nX));
+    CK(hipMalloc(&T0, 4 * nX));
+    CK(hipMalloc(&T1, 4 * nX));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipLaunchKernelGGL(fill, dim3((unsigned)((nW + 255) / 256)), dim3(256), 0, s, W, nW, 1u, 0.15f);
+    hipLaunchKernelGGL(fill, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, b, nb, 2u, 0.2f);
+    hipLaunchKernelGGL(fill, dim3((unsigned)((nX + 255) / 256)), dim3(256), 0, s, X, nX, 3u, 2.0f);
+    // reference chain
+    const float* in = X;
+    float* outs[2] = {T0, T1};
+    for (int l = 0; l < LAYERS; ++l) {
+        hipLaunchKernelGGL(ref_layer, dim3(ncols / 64, H, nm), dim3(64), 0, s, W, b, in, outs[l & 1], ncols, l);
+        in = outs[l & 1];
+    }
+    CK(hipStreamSynchronize(s));
+    std::vector<float> ref(nX);
+    CK(hipMemcpy(ref.data(), in, 4 * nX, hipMemcpyDeviceToHost));
+    run<8, 4, false>(nm, iters, W, b, X, Y, ref, ncols, s);
+    run<8, 4, true>(nm, iters, W, b, X, Y, ref, ncols, s);
+    run<8, 8, false>(nm, iters, W, b, X, Y, ref, ncols, s);
+    run<8, 8, true>(nm, iters, W, b, X, Y, ref, ncols, s);
+    run<16, 8, true>(nm, iters, W, b, X, Y, ref, ncols, s);
+    return 0;
+}

@@ -83,6 +83,9 @@ _SIGS = {
                                                    ctypes.POINTER(ctypes.c_double)]),
     "fqlpop_flops_per_member_step": (ctypes.c_double, [ctypes.POINTER(Config)]),
     "fqlpop_set_probe": (ctypes.c_int, [_P, ctypes.c_int]),
+    "fqlpop_dominant_kernel_info": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int,
+                                                   ctypes.POINTER(ctypes.c_double),
+                                                   ctypes.POINTER(ctypes.c_double)]),
     "fqlpop_read_probe": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                          ctypes.POINTER(ctypes.c_double)]),
 }

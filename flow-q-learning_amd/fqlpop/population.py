@@ -323,10 +323,18 @@ class Population:
         mean = tot.value / n.value if n.value else float("nan")
         return mean, int(n.value), (float(cc[0]), float(cc[1]))
 
+    def dominant_kernel_info(self):
+        """(kernel symbol, algorithmic FLOPs, unique HBM bytes) of one launch of
+        the step's dominant kernel over the active members."""
+        name = ctypes.create_string_buffer(128)
+        fl = ctypes.c_double()
+        by = ctypes.c_double()
+        check(self.lib.fqlpop_dominant_kernel_info(self._h, name, 128, ctypes.byref(fl), ctypes.byref(by)))
+        return name.value.decode(), float(fl.value), float(by.value)
+
     def dominant_kernel_flops(self) -> float:
         """Algorithmic FLOPs of one dominant-kernel launch (all active members)."""
-        H, B = self.cfg.hidden_dims[0], self.cfg.batch_size
-        return 2.0 * H * H * B * int(self.active.sum())
+        return self.dominant_kernel_info()[1]
 
     def time_dominant_kernel(self, iters: int = 50):
         us = ctypes.c_double()

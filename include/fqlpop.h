@@ -174,6 +174,10 @@ int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* 
  * if clock_check != NULL the last fqlpop_time_dominant_kernel cross-check:
  * [0] one isolated launch timed by HIP events, [1] the same by its stamps. */
 int fqlpop_set_probe(fqlpop_t* h, int enable);
+/* The dominant kernel of fqlpop_step (bench.py's roofline row): its kernel
+ * symbol (for profiler filters), algorithmic FLOPs and unique HBM bytes of one
+ * launch over the active members. */
+int fqlpop_dominant_kernel_info(fqlpop_t* h, char* name, int name_cap, double* flops, double* bytes);
 int fqlpop_read_probe(fqlpop_t* h, double* total_us, int64_t* launches, double* clock_check);
 
 /* Algorithmic GEMM FLOPs of one member-update at the handle's config

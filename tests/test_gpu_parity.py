@@ -108,6 +108,8 @@ def test_update_parity_q_min_normalized():
     (256, 128, dict(flow_steps=3, discount=0.995)),  # antsoccer reproduce discount
     (1024, 64, dict()),                           # widest supported hidden dim
     (64, 192, dict(q_agg="min", tau=0.05)),       # odd multiple of 64 rows
+    (512, 64, dict(flow_steps=3)),                # persistent Euler kernel, short flow
+    (512, 192, dict(layer_norm=False, q_agg="min")),  # persistent Euler kernel, 12 column tiles
 ])
 def test_update_parity_configs(H, B, kw):
     _run_parity(H, B, [4.0, 40.0], n_steps=2, **kw)
@@ -264,3 +266,15 @@ def test_set_active_subset_matches_full_population():
     assert np.array_equal(sub.get_flat(0), before0)
     assert np.array_equal(sub.get_flat(2), full.get_flat(2))
     assert sub.get_count(0) == 0 and sub.get_count(1) == 1
+
+
+def test_euler_fused_matches_per_layer_path(monkeypatch):
+    """The persistent Euler-flow kernel (H = 512) and the per-layer launches
+    give the same update to within fp32 reassociation."""
+    infos = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("FQLPOP_EULER", flag)
+        pop = _run_parity(512, 64, [25.0], n_steps=1)
+        infos.append(pop.read_info("train")[0])
+    for k in O.TRAIN_INFO_KEYS:
+        assert _close(infos[0][k], infos[1][k], rel=2e-5), (k, infos[0][k], infos[1][k])
