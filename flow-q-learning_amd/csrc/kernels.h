@@ -96,6 +96,35 @@ struct HeadArgs {         // out'[j][m] = sum_k W[k][j] h'[k][m] + b[j]
 };
 void launch_head_fwd(int mode, const HeadArgs& a, hipStream_t s);
 
+// ------------------------------------------------ streamed MLP forward ----
+// One launch = the whole forward pass of one network (every hidden layer with
+// its GELU / LayerNorm, and the head) for all active members and ensemble
+// members: a block owns 16 columns for all H = 512 features (slab in LDS),
+// weights stream from L2 (same k-loop as the Euler flow).  Stores the
+// activations the backward pass needs for columns [st_lo, st_hi), then calls
+// the head-mode epilogue of HeadArgs (head_write).
+struct StreamArgs {
+    const float* params;                  // arena + net offset (slot stride P, ensemble stride ens)
+    long long P, ens;
+    long long w_off[EF_MAX_LAYERS + 1], b_off[EF_MAX_LAYERS + 1];
+    long long g_off[EF_MAX_LAYERS], be_off[EF_MAX_LAYERS];  // LN scale / bias
+    const float* x0;                      // input [K0][ld_x] (+ slot * x0_ss), shared by ensemble members
+    long long x0_ss;
+    int ld_x, K0, L, M;
+    float* U[EF_MAX_LAYERS];              // pre-activation [H][ld_s] (+ slot*s_ss + y*s_sy), or null
+    float* G[EF_MAX_LAYERS];              // layer output (post GELU / LN) [H][ld_s], or null
+    float* MU[EF_MAX_LAYERS];             // LN mean [ld_s] (+ slot*st_ss + y*st_sy)
+    float* RS[EF_MAX_LAYERS];             // LN 1/sigma
+    long long s_ss, s_sy, st_ss, st_sy;
+    int ld_s, st_lo, st_hi;
+    HeadArgs head;                        // head outputs (head.M/.ld unused)
+    int ny, nz;
+    const int* slots;
+};
+bool stream_fwd_supported(int H, int L, int K0, int nout, int M);
+void launch_stream_fwd(int head_mode, bool ln, const StreamArgs& a, hipStream_t s);
+
+
 struct BwdArgs {
     TRef dh;              // [H][ld_d] gradient w.r.t. layer output (non-head mode)
     TRef dout, W5;        // head mode: dout'[nout][ld_o], W5[H][nout]

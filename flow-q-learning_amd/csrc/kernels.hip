@@ -537,6 +537,35 @@ DEV float gelu_fast(float x) {
     return 0.5f * x * (1.0f + t);
 }
 
+// One streamed layer's k-loop: acc[c] += W[k][64w + 4li + c] * xs[k][li] over
+// k < 4 NS (NS a multiple of EF_PF).  ring[] holds the next EF_PF k-steps' A
+// fragments on entry; on exit it holds the first EF_PF of the layer at
+// w_next (element offset of the next layer's Dense kernel).
+DEV void ef_kloop(f32x4 (&acc)[4], float4 (&ring)[EF_PF], rsrc_t rW, const float* xs, int NS, int w_cur,
+                  int w_next, int lo, int lk, int li) {
+    constexpr int H = EF_H, NC = EF_NC, PF = EF_PF;
+    float bnext = xs[lk * NC + li];
+    for (int s0 = 0; s0 < NS; s0 += PF) {
+        // refill targets: k-steps s0+PF.. of this layer, or the next layer's first PF
+        const int rbase = (s0 + PF < NS ? w_cur + 4 * (s0 + PF) * H : w_next) + lo;
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            const int s = s0 + p;
+            const float b = bnext;
+            bnext = xs[(4 * (s + 1) + lk) * NC + li];  // one k-step ahead (past the end: unused)
+            __builtin_amdgcn_sched_barrier(0);
+            const float4 a = ring[p];
+            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b, acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b, acc[1], 0, 0, 0);
+            acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b, acc[2], 0, 0, 0);
+            acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b, acc[3], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            ring[p] = bload4(rW, rbase + 4 * p * H);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
 bool euler_flow_supported(int H, int L, int D, int A, int B) {
     return H == EF_H && L >= 1 && L <= EF_MAX_LAYERS && D + A + 1 <= EF_K0MAX && A <= 8 && B % EF_NC == 0;
 }
@@ -596,26 +625,7 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
             float4 bias4[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) bias4[r] = bload4(rW, (int)g.b_off[l] + 64 * w + 16 * lk + 4 * r);
-            float bnext = xs[lk * NC + li];
-            for (int s0 = 0; s0 < NS; s0 += PF) {
-                // refill targets: k-steps s0+PF.. of this layer, or the next layer's first PF
-                const int rbase = (s0 + PF < NS ? (int)g.w_off[l] + 4 * (s0 + PF) * H : (int)g.w_off[nl]) + lo;
-#pragma unroll
-                for (int p = 0; p < PF; ++p) {
-                    const int s = s0 + p;
-                    const float b = bnext;
-                    bnext = xs[(4 * (s + 1) + lk) * NC + li];  // one k-step ahead (past the end: unused)
-                    __builtin_amdgcn_sched_barrier(0);
-                    const float4 a = ring[p];
-                    acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b, acc[0], 0, 0, 0);
-                    acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b, acc[1], 0, 0, 0);
-                    acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b, acc[2], 0, 0, 0);
-                    acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b, acc[3], 0, 0, 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    ring[p] = bload4(rW, rbase + 4 * p * H);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
+            ef_kloop(acc, ring, rW, xs, NS, (int)g.w_off[l], (int)g.w_off[nl], lo, lk, li);
             // tile c, reg r, lane (lk, li): feature 64w + 4(4lk + r) + c, column li
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -847,6 +857,180 @@ void launch_head_fwd(int mode, const HeadArgs& a, hipStream_t s) {
         case HEAD_OS: FQ_KPT_DISPATCH(a.H, FQ_HEAD_LAUNCH, HEAD_OS, grid, s, a) break;
         default: FQ_KPT_DISPATCH(a.H, FQ_HEAD_LAUNCH, HEAD_ACT, grid, s, a) break;
     }
+}
+
+// ===================================================== streamed MLP forward ==
+// The whole forward pass of one network in one launch (StreamArgs, kernels.h):
+// block = 16 columns x all 512 features of one (member, ensemble member); the
+// same weight-streaming k-loop as the Euler flow.  One LDS slab holds the
+// layer input; after a barrier (every wave done reading it) the epilogue
+// overwrites it with the layer output, so LDS stays ~38 KB and blocks of other
+// kernels fit beside this one.  Epilogue per hidden layer: u = acc + b
+// (stored if requested), g = gelu(u), LayerNorm over the 512 features of each
+// column when LN (statistics: lane partials -> shuffles over lk -> LDS over
+// the 8 waves), layer output stored if requested and written to the slab.
+// The head (nout <= 8) is a 16x16x4 MFMA per wave over its 64 features,
+// reduced over waves in LDS, and handed to head_write<MODE>.
+bool stream_fwd_supported(int H, int L, int K0, int nout, int M) {
+    return H == EF_H && L >= 1 && L <= EF_MAX_LAYERS && K0 <= EF_K0MAX && nout <= 8 && M % EF_NC == 0;
+}
+
+template <int MODE, bool LN>
+__global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamArgs g) {
+    constexpr int H = EF_H, NC = EF_NC, NT = EF_NW * 64, PF = EF_PF;
+    __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];          // + slack for the look-ahead read
+    __shared__ __attribute__((aligned(16))) float in0[EF_K0MAX * NC + 64];   // layer-0 input, then head partials
+    __shared__ float lnred[2][EF_NW][NC];
+    __shared__ float lnp[3][H];  // this layer's bias, LN scale, LN bias
+
+    const int tiles = g.M / NC;
+    const int total = tiles * g.ny * g.nz;
+    const int bid = xcd_remap(blockIdx.x, total);
+    const int tile = bid % tiles, yz = bid / tiles;
+    const int y = yz % g.ny, z = yz / g.ny;
+    const int slot = g.slots[z];
+    const int c0 = tile * NC;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    const int L = g.L, K0 = g.K0, nout = g.head.nout;
+    const int NS0 = (K0 + 4 * PF - 1) / (4 * PF) * PF;
+    const float* __restrict__ P = g.params + (long long)slot * g.P + (long long)y * g.ens;
+    const float* __restrict__ x0 = g.x0 + (long long)slot * g.x0_ss;
+    for (int e = tid; e < EF_K0MAX * NC + 64; e += NT) {
+        const int r = e / NC, j = e % NC;
+        in0[e] = r < K0 ? x0[(long long)r * g.ld_x + c0 + j] : 0.f;
+    }
+    const rsrc_t rW = make_rsrc(P, g.P);
+    const int lo = lk * H + 64 * w + 4 * li;
+    float4 ring[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) ring[p] = bload4(rW, (int)g.w_off[0] + 4 * p * H + lo);
+    const bool st = c0 >= g.st_lo && c0 + NC <= g.st_hi;  // block stores activations
+    const int m = c0 + li;
+    __syncthreads();
+
+    for (int l = 0; l < L; ++l) {
+        const int NS = l == 0 ? NS0 : H / 4;
+        const float* xs = l == 0 ? in0 : slab;
+        const int nl = l + 1 < L ? l + 1 : 0;
+        f32x4 acc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // this lane's 16 features 64w + 16lk + 4r + c: bias (and LN scale / bias) in flight during the k-loop
+        // feature tid's bias / LN scale / LN bias, in flight during the k-loop, then to LDS
+        const float pb = P[g.b_off[l] + tid];
+        const float pg = LN ? P[g.g_off[l] + tid] : 0.f;
+        const float pe = LN ? P[g.be_off[l] + tid] : 0.f;
+        ef_kloop(acc, ring, rW, xs, NS, (int)g.w_off[l], (int)g.w_off[nl], lo, lk, li);
+        lnp[0][tid] = pb;
+        if constexpr (LN) {
+            lnp[1][tid] = pg;
+            lnp[2][tid] = pe;
+        }
+        __syncthreads();  // every wave is done reading the slab; lnp visible
+
+        float* __restrict__ U = st && g.U[l] ? g.U[l] + (long long)slot * g.s_ss + (long long)y * g.s_sy : nullptr;
+        float* __restrict__ G = st && g.G[l] ? g.G[l] + (long long)slot * g.s_ss + (long long)y * g.s_sy : nullptr;
+        float v[4][4];  // [r][c]: feature 64w + 16lk + 4r + c, column li
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float4 bb = *reinterpret_cast<const float4*>(&lnp[0][64 * w + 16 * lk + 4 * r]);
+            const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float u = acc[c][r] + bv[c];
+                if (U) U[(long long)(64 * w + 16 * lk + 4 * r + c) * g.ld_s + m] = u;
+                v[r][c] = gelu_fast(u);
+            }
+        }
+        if constexpr (LN) {
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    s1 += v[r][c];
+                    s2 += v[r][c] * v[r][c];
+                }
+            s1 += __shfl_xor(s1, 16, 64);
+            s2 += __shfl_xor(s2, 16, 64);
+            s1 += __shfl_xor(s1, 32, 64);
+            s2 += __shfl_xor(s2, 32, 64);
+            if (lk == 0) {
+                lnred[0][w][li] = s1;
+                lnred[1][w][li] = s2;
+            }
+            __syncthreads();
+            float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < EF_NW; ++q) {
+                S1 += lnred[0][q][li];
+                S2 += lnred[1][q][li];
+            }
+            const float mean = S1 / (float)H;
+            const float var = fmaxf(S2 / (float)H - mean * mean, 0.f);
+            const float rs = 1.0f / sqrtf(var + 1e-6f);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float4 g4 = *reinterpret_cast<const float4*>(&lnp[1][64 * w + 16 * lk + 4 * r]);
+                const float4 b4 = *reinterpret_cast<const float4*>(&lnp[2][64 * w + 16 * lk + 4 * r]);
+                const float ga[4] = {g4.x, g4.y, g4.z, g4.w};
+                const float be[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) v[r][c] = (v[r][c] - mean) * rs * ga[c] + be[c];
+            }
+            if (st && w == 0 && lk == 0 && g.MU[l]) {
+                const long long so = (long long)slot * g.st_ss + (long long)y * g.st_sy + m;
+                g.MU[l][so] = mean;
+                g.RS[l][so] = rs;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int f = 64 * w + 16 * lk + 4 * r + c;
+                if (G) G[(long long)f * g.ld_s + m] = v[r][c];
+                slab[f * NC + li] = v[r][c];
+            }
+        __syncthreads();
+    }
+    // head: out[j][col] = sum_k W_L[k][j] h[k][col] + b_L[j]
+    {
+        float w5r[16];  // A fragments: W_L[64w + 4s + lk][li], li < nout
+#pragma unroll
+        for (int s = 0; s < 16; ++s) w5r[s] = li < nout ? P[g.w_off[L] + (64 * w + 4 * s + lk) * nout + li] : 0.f;
+        f32x4 hacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+            hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(w5r[s], slab[(64 * w + 4 * s + lk) * NC + li], hacc, 0, 0, 0);
+        float* hred = in0;  // [EF_NW][8 x NC]
+        if (lk < 2) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hred[w * 8 * NC + (4 * lk + r) * NC + li] = hacc[r];
+        }
+        __syncthreads();
+        if (tid < nout * NC) {
+            const int j = tid / NC, col = tid % NC;
+            float v = hred[tid];
+#pragma unroll
+            for (int q = 1; q < EF_NW; ++q) v += hred[q * 8 * NC + tid];
+            v += P[g.b_off[L] + j];
+            head_write<MODE>(g.head, slot, y, j, c0 + col, v);
+        }
+    }
+}
+
+void launch_stream_fwd(int head_mode, bool ln, const StreamArgs& a, hipStream_t s) {
+    const dim3 grid((a.M / EF_NC) * a.ny * a.nz), block(EF_NW * 64);
+#define FQ_SF(MODE, LNV) hipLaunchKernelGGL((stream_fwd_kernel<MODE, LNV>), grid, block, 0, s, a)
+    switch (head_mode) {
+        case HEAD_BC_FUSED: if (ln) FQ_SF(HEAD_BC_FUSED, true); else FQ_SF(HEAD_BC_FUSED, false); break;
+        case HEAD_OS: if (ln) FQ_SF(HEAD_OS, true); else FQ_SF(HEAD_OS, false); break;
+        default: if (ln) FQ_SF(HEAD_STORE, true); else FQ_SF(HEAD_STORE, false); break;
+    }
+#undef FQ_SF
 }
 
 // ============================================================ backward =====

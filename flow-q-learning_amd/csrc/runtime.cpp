@@ -166,6 +166,7 @@ struct fqlpop {
     // its blocks stamp s_memrealtime into per-launch slots; two slot sets are
     // used by alternate steps so the host reads step i-2 while step i runs
     bool euler_fused = false;      // Euler steps 1..S-1 as one persistent launch (euler_flow_kernel)
+    bool stream_fwd = false;       // whole-network forward launches (stream_fwd_kernel)
     bool probe = false;
     int probe_set = -1;            // set used by the step being enqueued (-1: none)
     int probe_idx = 0;             // next launch slot of that set
@@ -511,6 +512,44 @@ void adam_net(const Ctx& c, hipStream_t s, int ni) {
     launch_adam(a, s);
 }
 
+// One whole-network forward launch (stream_fwd_kernel).  `arena` + N.off is the
+// net's parameter block (slot stride P); activations for the backward pass are
+// stored for columns [st_lo, st_hi) into U/G (slot stride s_ss, ensemble
+// stride s_sy, leading dim ld_s) and MU/RS (st_ss, st_sy) when given.
+void stream_fwd(const Ctx& c, hipStream_t s, const NetLayout& N, const float* arena, long long P, TRef X, int ldx,
+                int M, const std::vector<float*>* U, const std::vector<float*>* G, const std::vector<float*>* MU,
+                const std::vector<float*>* RS, long long s_ss, long long s_sy, long long st_ss, long long st_sy,
+                int st_lo, int st_hi, int mode, const HeadArgs& head) {
+    fqlpop* h = c.h;
+    StreamArgs a{};
+    a.params = arena + N.off;
+    a.P = P;
+    a.ens = N.ens_size;
+    for (int l = 0; l <= N.L; ++l) {
+        a.w_off[l] = N.W[l];
+        a.b_off[l] = N.b[l];
+        if (l < N.L && N.ln) {
+            a.g_off[l] = N.gam[l];
+            a.be_off[l] = N.bet[l];
+        }
+        if (l < N.L) {
+            a.U[l] = U ? (*U)[l] : nullptr;
+            a.G[l] = G ? (*G)[l] : nullptr;
+            a.MU[l] = MU ? (*MU)[l] : nullptr;
+            a.RS[l] = RS ? (*RS)[l] : nullptr;
+        }
+    }
+    a.x0 = X.p;
+    a.x0_ss = X.ss;
+    a.ld_x = ldx; a.K0 = N.in_dim; a.L = N.L; a.M = M;
+    a.s_ss = s_ss; a.s_sy = s_sy; a.st_ss = st_ss; a.st_sy = st_sy;
+    a.ld_s = ldx; a.st_lo = st_lo; a.st_hi = st_hi;
+    a.head = head;
+    a.head.nout = N.out_dim;
+    a.ny = N.E; a.nz = c.nz; a.slots = h->slots;
+    launch_stream_fwd(mode, N.ln, a, s);
+}
+
 // Arguments of the persistent Euler-flow launch: steps 1..S-1 from eu_in (the
 // state the BC head left after step 0) to aflow.
 EulerArgs euler_args(fqlpop* h, int nz) {
@@ -605,14 +644,20 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     // ---- sF: BC-flow forward (train rows) fused with Euler step 0 --------
     {
         const NetLayout& N = h->bc;
-        fwd_hidden(c, sF, N, tref(h->bc_in, (long long)Kb * B2), B2, B2, h->bc_u, h->bc_g, 0,
-                   nullptr, nullptr, 0, true);
         HeadArgs ha = head_args(c, N, h->bc_g[L - 1], B2, B2, 0);
         ha.o0 = tref(h->vpred, (long long)A * B); ha.ld0 = B;
         ha.o1 = tref(h->bc_in, (long long)Kb * B2); ha.ld1 = B2;
         ha.o2 = tref(h->eu_in, (long long)Kb * B); ha.ld2 = B;
         ha.t_next = (float)(1.0 / (double)S);
-        launch_head_fwd(HEAD_BC_FUSED, ha, sF);
+        if (h->stream_fwd) {
+            // train rows [0, B) feed the BC backward; rows [B, 2B) are Euler step 0
+            stream_fwd(c, sF, N, h->params, h->P, tref(h->bc_in, (long long)Kb * B2), B2, B2, &h->bc_u, &h->bc_g,
+                       nullptr, nullptr, (long long)H * B2, 0, 0, 0, 0, B, HEAD_BC_FUSED, ha);
+        } else {
+            fwd_hidden(c, sF, N, tref(h->bc_in, (long long)Kb * B2), B2, B2, h->bc_u, h->bc_g, 0,
+                       nullptr, nullptr, 0, true);
+            launch_head_fwd(HEAD_BC_FUSED, ha, sF);
+        }
         HIPCHK(hipEventRecord(h->ev_bcfwd, sF));
         if (h->euler_fused) {
             EulerArgs ea = euler_args(h, c.nz);
@@ -657,20 +702,32 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     // ---- sM: one-step actor forward on [s'; s; s] (z_next; z_d; z_metric) --
     {
         const NetLayout& N = h->os;
-        fwd_hidden(c, sM, N, tref(h->os_in, (long long)Kc * B3), B3, B3, h->os_u, h->os_g, 0,
-                   nullptr, nullptr, 0, true);
         HeadArgs ha = head_args(c, N, h->os_g[L - 1], B3, B3, 0);
         ha.o0 = tref(h->apiraw, (long long)A * B); ha.ld0 = B;
         ha.o1 = tref(h->tg_in, (long long)Kc * B); ha.ld1 = B;
         ha.o2 = tref(h->cr_in, (long long)Kc * B2); ha.ld2 = B2;
         ha.o3 = tref(h->amet, (long long)A * B); ha.ld3 = B;
-        launch_head_fwd(HEAD_OS, ha, sM);
+        if (h->stream_fwd) {
+            // only the z_d rows [B, 2B) are back-propagated (distill + Q loss)
+            stream_fwd(c, sM, N, h->params, h->P, tref(h->os_in, (long long)Kc * B3), B3, B3, &h->os_u, &h->os_g,
+                       nullptr, nullptr, (long long)H * B3, 0, 0, 0, B, 2 * B, HEAD_OS, ha);
+        } else {
+            fwd_hidden(c, sM, N, tref(h->os_in, (long long)Kc * B3), B3, B3, h->os_u, h->os_g, 0,
+                       nullptr, nullptr, 0, true);
+            launch_head_fwd(HEAD_OS, ha, sM);
+        }
     }
     dep(sM, sX);  // a' is in the target-critic input
     const NetLayout& NC = h->critic;
     const long long sy2 = (long long)H * B2, sy1 = (long long)H * B;
     // ---- sX: target critic on [s', a'] (params from the target arena) -----
-    {
+    if (h->stream_fwd) {
+        HeadArgs ht{};
+        ht.B = B; ht.D = D; ht.steps_f = (float)S;
+        ht.o0 = tref(h->qt, (long long)E * B, B); ht.ld0 = B;
+        stream_fwd(c, sX, NC, h->target, h->PT, tref(h->tg_in, (long long)Kc * B), B, B, nullptr, nullptr, nullptr,
+                   nullptr, 0, 0, 0, 0, 0, 0, HEAD_STORE, ht);
+    } else {
         const NetLayout& N = NC;
         for (int l = 0; l < L; ++l) {
             GemmArgs g{};
@@ -706,11 +763,17 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     // ---- sM: critic on [s,a ; s,clip(a_pi)] -------------------------------
     {
         const NetLayout& N = NC;
-        fwd_hidden(c, sM, N, tref(h->cr_in, (long long)Kc * B2, 0), B2, B2, h->cr_u, h->cr_h, sy2,
-                   &h->cr_mu, &h->cr_rs, B2, true);
         HeadArgs hc = head_args(c, N, h->cr_h[L - 1], B2, B2, sy2);
         hc.o0 = tref(h->q, (long long)E * B2, B2); hc.ld0 = B2;
-        launch_head_fwd(HEAD_STORE, hc, sM);
+        if (h->stream_fwd) {
+            stream_fwd(c, sM, N, h->params, h->P, tref(h->cr_in, (long long)Kc * B2, 0), B2, B2, &h->cr_u, &h->cr_h,
+                       N.ln ? &h->cr_mu : nullptr, N.ln ? &h->cr_rs : nullptr, (long long)H * B2 * E, sy2,
+                       (long long)B2 * E, B2, 0, B2, HEAD_STORE, hc);
+        } else {
+            fwd_hidden(c, sM, N, tref(h->cr_in, (long long)Kc * B2, 0), B2, B2, h->cr_u, h->cr_h, sy2,
+                       &h->cr_mu, &h->cr_rs, B2, true);
+            launch_head_fwd(HEAD_STORE, hc, sM);
+        }
     }
     dep(sX, sM);  // Q_target
     launch_loss_critic(la, sM);
@@ -897,9 +960,24 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         h->PT = align_up(h->critic.size());
         build_leaves(h.get());
 
-        HIPCHK(hipStreamCreateWithFlags(&h->sM, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&h->sF, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
+        // Stream priorities (FQLPOP_PRIO, experiment switch): 0 = all default
+        // (measured fastest), 1 = main chain high, 2 = Euler flow high.
+        {
+            int least = 0, greatest = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            const char* pe = std::getenv("FQLPOP_PRIO");
+            const int mode = pe ? std::atoi(pe) : 0;
+            HIPCHK(hipStreamCreateWithPriority(&h->sM, hipStreamNonBlocking, mode == 1 ? greatest : 0));
+            HIPCHK(hipStreamCreateWithPriority(&h->sF, hipStreamNonBlocking, mode == 2 ? greatest : 0));
+            HIPCHK(hipStreamCreateWithPriority(&h->sB, hipStreamNonBlocking, mode == 1 ? least : 0));
+        }
+        // FQLPOP_SERIAL=1 (profiling switch): every kernel of the step on sM, so a
+        // kernel trace shows uncontended durations
+        bool serial = false;
+        {
+            const char* se = std::getenv("FQLPOP_SERIAL");
+            serial = se && std::atoi(se) == 1;
+        }
         // A 4th stream (target critic + dW GEMMs + Adams off the main chain) is
         // opt-in: on MI355X the step is throughput-bound and the extra
         // concurrency measured 5% slower.
@@ -908,10 +986,20 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             if (ns && std::atoi(ns) >= 4) HIPCHK(hipStreamCreateWithFlags(&h->sX, hipStreamNonBlocking));
             else h->sX = h->sM;
         }
+        if (serial) {
+            HIPCHK(hipStreamDestroy(h->sF));
+            HIPCHK(hipStreamDestroy(h->sB));
+            if (h->sX != h->sM) HIPCHK(hipStreamDestroy(h->sX));
+            h->sF = h->sB = h->sX = h->sM;
+        }
         h->ev_pool.resize(64);
         {
             const char* ef = std::getenv("FQLPOP_EULER");
             h->euler_fused = euler_flow_supported(H, L, D, A, B) && !h->bc.ln && !(ef && std::atoi(ef) == 0);
+        }
+        {
+            const char* sf = std::getenv("FQLPOP_STREAM");
+            h->stream_fwd = stream_fwd_supported(H, L, D + A + 1, A, B) && !(sf && std::atoi(sf) == 0);
         }
         if (h->euler_fused) {  // dominant kernel: one persistent Euler launch per step
             h->probe_pairs = 1;
@@ -1023,8 +1111,9 @@ int fqlpop_destroy(fqlpop_t* h) {
         if (h->probe_stream) (void)hipStreamDestroy(h->probe_stream);
         if (h->probe_slots) (void)hipFree(h->probe_slots);
         if (h->sX && h->sX != h->sM) (void)hipStreamDestroy(h->sX);
-        for (hipStream_t s : {h->sM, h->sF, h->sB})
-            if (s) (void)hipStreamDestroy(s);
+        if (h->sF && h->sF != h->sM) (void)hipStreamDestroy(h->sF);
+        if (h->sB && h->sB != h->sM) (void)hipStreamDestroy(h->sB);
+        if (h->sM) (void)hipStreamDestroy(h->sM);
         delete h;
     });
 }

@@ -130,6 +130,239 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp_stream16(const float* __restri
     }
 }
 
+// CG column groups of 16 per block (NC = 16 CG): one W fragment feeds CG MFMA
+// sets, halving W traffic per FLOP at CG = 2.  8 waves, single slab (the
+// epilogue overwrites the input after a barrier).
+template <int PF, int CG, int MODE>
+__global__ __launch_bounds__(512, 1) void mlp_stream_cg(const float* __restrict__ W, const float* __restrict__ bias,
+                                                        const float* __restrict__ X, float* __restrict__ Y,
+                                                        int ncols) {
+    constexpr int NCT = 16 * CG, NT = 512;
+    __shared__ __attribute__((aligned(16))) float slab[H * NCT + 64];
+    const int tiles = ncols / NCT;
+    const int total = gridDim.x, q = total >> 3, rr = total & 7, x = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int bid = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + loc;
+    const int m = bid / tiles, c0 = (bid % tiles) * NCT;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    for (int e = tid; e < H * NCT; e += NT) {
+        const int f = e / NCT, j = e % NCT;
+        slab[e] = X[((long long)m * H + f) * ncols + c0 + j];
+    }
+    const rsrc_t rW = make_rsrc(W + (long long)m * LAYERS * H * H, (long long)LAYERS * H * H);
+    const int lo = lk * H + 64 * w + 4 * li;
+    constexpr int NS = H / 4;
+    float4 ring[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) ring[p] = bload4(rW, lo + 4 * p * H);
+    __syncthreads();
+    for (int l = 0; l < LAYERS; ++l) {
+        f32x4 acc[CG][4];
+#pragma unroll
+        for (int g = 0; g < CG; ++g)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float4 bias4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bias4[r] = *reinterpret_cast<const float4*>(bias + ((long long)m * LAYERS + l) * H + 64 * w + 16 * lk + 4 * r);
+        const int lbase = lo + l * H * H;
+        float bnext[CG];
+#pragma unroll
+        for (int g = 0; g < CG; ++g) bnext[g] = slab[lk * NCT + 16 * g + li];
+        for (int s0 = 0; s0 < NS; s0 += PF) {
+#pragma unroll
+            for (int p = 0; p < PF; ++p) {
+                const int s = s0 + p;
+                float b[CG];
+#pragma unroll
+                for (int g = 0; g < CG; ++g) {
+                    b[g] = bnext[g];
+                    bnext[g] = slab[(4 * (s + 1) + lk) * NCT + 16 * g + li];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const float4 a = ring[p];
+#pragma unroll
+                for (int g = 0; g < CG; ++g) {
+                    if (MODE == 2) { acc[g][0][0] += a.x * b[g] + a.y + a.z + a.w; continue; }
+                    acc[g][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[g], acc[g][0], 0, 0, 0);
+                    acc[g][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[g], acc[g][1], 0, 0, 0);
+                    acc[g][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[g], acc[g][2], 0, 0, 0);
+                    acc[g][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[g], acc[g][3], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                // MODE 1: no weight loads (MFMA + LDS ceiling); MODE 2: loads only
+                if (MODE != 1) ring[p] = bload4(rW, lbase + 4 * (s + PF) * H);
+                else ring[p].x += 1e-9f;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < CG; ++g)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float bb[4] = {bias4[r].x, bias4[r].y, bias4[r].z, bias4[r].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int f = 64 * w + 16 * lk + 4 * r + c;
+                    slab[f * NCT + 16 * g + li] = gelu_fast(acc[g][c][r] + bb[c]);
+                }
+            }
+        __syncthreads();
+    }
+    for (int e = tid; e < H * NCT; e += NT) {
+        const int f = e / NCT, j = e % NCT;
+        Y[((long long)m * H + f) * ncols + c0 + j] = slab[e];
+    }
+}
+
+// Transposed-access (dX) streaming: Y[k][m] = sum_i W[k][i] X[i][m] (W row-major
+// [k][i], the flax kernel read along its output index i = the reduction).
+// Wave w owns output rows 64w .. 64w+63 as 4 tiles of 16; a k-step covers 16
+// reduction indices: lane (li, lk) loads float4 W[64w + 16t + li][16s + 4lk ..],
+// component c is MFMA c's reduction index 16s + 4lk + c, B = X[16s + 4lk + c][li].
+template <int PF>
+__global__ __launch_bounds__(512, 1) void dx_stream(const float* __restrict__ W, const float* __restrict__ bias,
+                                                    const float* __restrict__ X, float* __restrict__ Y, int ncols) {
+    constexpr int NC = 16, NT = 512;
+    __shared__ __attribute__((aligned(16))) float slab[H * NC + 256];
+    const int tiles = ncols / NC;
+    const int total = gridDim.x, q = total >> 3, rr = total & 7, x = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int bid = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + loc;
+    const int m = bid / tiles, c0 = (bid % tiles) * NC;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    for (int e = tid; e < H * NC; e += NT) {
+        const int f = e / NC, j = e % NC;
+        slab[e] = X[((long long)m * H + f) * ncols + c0 + j];
+    }
+    const rsrc_t rW = make_rsrc(W + (long long)m * LAYERS * H * H, (long long)LAYERS * H * H);
+    constexpr int NS = H / 16;
+    float4 ring[PF][4];
+    const int lo = (64 * w + li) * H + 4 * lk;  // + 16 t H + 16 s
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) ring[p][t] = bload4(rW, lo + 16 * t * H + 16 * p);
+    __syncthreads();
+    for (int l = 0; l < LAYERS; ++l) {
+        f32x4 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int lbase = lo + l * H * H;
+        float bn[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bn[c] = slab[(4 * lk + c) * NC + li];
+        for (int s0 = 0; s0 < NS; s0 += PF) {
+#pragma unroll
+            for (int p = 0; p < PF; ++p) {
+                const int s = s0 + p;
+                float b[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    b[c] = bn[c];
+                    bn[c] = slab[(16 * (s + 1) + 4 * lk + c) * NC + li];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float4 a = ring[p][t];
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[0], acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[1], acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[2], acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[3], acc[t], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) ring[p][t] = bload4(rW, lbase + 16 * t * H + 16 * (s + PF));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        __syncthreads();
+        // tile t, reg r, lane (lk, li): row 64w + 16t + 4lk + r, column li
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int f = 64 * w + 16 * t + 4 * lk + r;
+                slab[f * NC + li] = gelu_fast(acc[t][r] + bias[((long long)m * LAYERS + l) * H + f]);
+            }
+        __syncthreads();
+    }
+    for (int e = tid; e < H * NC; e += NT) {
+        const int f = e / NC, j = e % NC;
+        Y[((long long)m * H + f) * ncols + c0 + j] = slab[e];
+    }
+}
+
+__global__ void ref_layer_t(const float* W, const float* bias, const float* X, float* Y, int ncols, int l) {
+    const int m = blockIdx.z, k = blockIdx.y, j = blockIdx.x * 64 + threadIdx.x;
+    if (j >= ncols) return;
+    const float* Wl = W + ((long long)m * LAYERS + l) * H * H;
+    float s = 0.f;
+    for (int i = 0; i < H; ++i) s = fmaf(Wl[(long long)k * H + i], X[((long long)m * H + i) * ncols + j], s);
+    Y[((long long)m * H + k) * ncols + j] = gelu_f(s + bias[((long long)m * LAYERS + l) * H + k]);
+}
+
+template <int PF>
+void run_dx(int nm, int iters, const float* W, const float* b, const float* X, float* Y, float* T0, float* T1,
+            int ncols, hipStream_t s) {
+    const long long nX = (long long)nm * H * ncols;
+    const float* in = X;
+    float* outs[2] = {T0, T1};
+    for (int l = 0; l < LAYERS; ++l) {
+        hipLaunchKernelGGL(ref_layer_t, dim3(ncols / 64, H, nm), dim3(64), 0, s, W, b, in, outs[l & 1], ncols, l);
+        in = outs[l & 1];
+    }
+    CK(hipStreamSynchronize(s));
+    std::vector<float> ref(nX), got(nX);
+    CK(hipMemcpy(ref.data(), in, 4 * nX, hipMemcpyDeviceToHost));
+    const dim3 grid(nm * (ncols / 16));
+    hipLaunchKernelGGL((dx_stream<PF>), grid, dim3(512), 0, s, W, b, X, Y, ncols);
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(got.data(), Y, 4 * nX, hipMemcpyDeviceToHost));
+    double err = 0;
+    for (long long i = 0; i < nX; ++i) err = std::max(err, (double)std::fabs(got[i] - ref[i]));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((dx_stream<PF>), grid, dim3(512), 0, s, W, b, X, Y, ncols);
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1000.0 * ms / iters;
+    const double fl = 2.0 * H * H * (double)ncols * nm * LAYERS;
+    std::printf("dx_stream PF=%d members %d cols %d: %8.2f us per 3 layers  %7.2f TFLOP/s  maxerr %.2e\n", PF, nm,
+                ncols, us, fl / us / 1e6, err);
+}
+
+template <int PF, int CG, int MODE>
+void run_cg(int nm, int iters, const float* W, const float* b, const float* X, float* Y,
+            const std::vector<float>& ref, int ncols, hipStream_t s) {
+    const dim3 grid(nm * (ncols / (16 * CG)));
+    hipLaunchKernelGGL((mlp_stream_cg<PF, CG, MODE>), grid, dim3(512), 0, s, W, b, X, Y, ncols);
+    CK(hipStreamSynchronize(s));
+    std::vector<float> got(ref.size());
+    CK(hipMemcpy(got.data(), Y, sizeof(float) * got.size(), hipMemcpyDeviceToHost));
+    double err = 0;
+    for (size_t i = 0; i < got.size(); ++i) err = std::max(err, (double)std::fabs(got[i] - ref[i]));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((mlp_stream_cg<PF, CG, MODE>), grid, dim3(512), 0, s, W, b, X, Y, ncols);
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1000.0 * ms / iters;
+    const double fl = 2.0 * H * H * (double)ncols * nm * LAYERS;
+    std::printf("stream_cg MODE=%d CG=%d PF=%d members %d cols %d: %8.2f us per 3 layers  %7.2f TFLOP/s  maxerr %.2e\n", MODE, CG,
+                PF, nm, ncols, us, fl / us / 1e6, err);
+}
+
 __global__ void ref_layer(const float* W, const float* bias, const float* X, float* Y, int ncols, int l) {
     const int m = blockIdx.z, i = blockIdx.y, j = blockIdx.x * 64 + threadIdx.x;
     if (j >= ncols) return;
@@ -175,7 +408,7 @@ void run(int nm, int iters, const float* W, const float* b, const float* X, floa
 int main(int argc, char** argv) {
     const int nm = argc > 1 ? std::atoi(argv[1]) : 16;
     const int iters = argc > 2 ? std::atoi(argv[2]) : 20;
-    const int ncols = 256;
+    const int ncols = argc > 3 ? std::atoi(argv[3]) : 256;
     const long long nW = (long long)nm * LAYERS * H * H, nb = (long long)nm * LAYERS * H,
                     nX = (long long)nm * H * ncols;
     float *W, *b, *X, *Y, *T0, *T1;
@@ -200,10 +433,8 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s));
     std::vector<float> ref(nX);
     CK(hipMemcpy(ref.data(), in, 4 * nX, hipMemcpyDeviceToHost));
-    run<8, 4, false>(nm, iters, W, b, X, Y, ref, ncols, s);
-    run<8, 4, true>(nm, iters, W, b, X, Y, ref, ncols, s);
-    run<8, 8, false>(nm, iters, W, b, X, Y, ref, ncols, s);
-    run<8, 8, true>(nm, iters, W, b, X, Y, ref, ncols, s);
-    run<16, 8, true>(nm, iters, W, b, X, Y, ref, ncols, s);
+    run_cg<8, 1, 0>(nm, iters, W, b, X, Y, ref, ncols, s);
+    run_dx<2>(nm, iters, W, b, X, Y, T0, T1, ncols, s);
+    run_dx<4>(nm, iters, W, b, X, Y, T0, T1, ncols, s);
     return 0;
 }
