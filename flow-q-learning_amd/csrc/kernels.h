@@ -124,6 +124,75 @@ struct StreamArgs {
 bool stream_fwd_supported(int H, int L, int K0, int nout, int M);
 void launch_stream_fwd(int head_mode, bool ln, const StreamArgs& a, hipStream_t s);
 
+// ----------------------------------------------- streamed MLP backward ----
+// One launch = the whole dX chain of one network for all active members and
+// ensemble members: from the head-output gradient dout through every hidden
+// layer (GELU', LayerNorm backward) down to du_0.  A block owns 16 columns and
+// all H = 512 features; du_l stays in LDS as the A operand of the next
+// layer's dh = W du (weights streamed from L2).  Writes du_l [H][ld_d] for the
+// dW GEMMs and, for columns < Mg, per-block column sums of du (bias grads), of
+// dh * xhat and dh (LN scale / bias grads) and of G_{L-1} dout (head kernel
+// grad) into `part` [tile][NP]; colsum_reduce folds the tiles into the grads.
+struct StreamBwdArgs {
+    const float* params;                  // arena + net offset (slot stride P, ensemble stride ens)
+    long long P, ens;
+    const float* paramsT;                 // transposed hidden kernels W_l^T [out][in] (slot stride PT, ens stride ensT)
+    long long PT, ensT;
+    long long wt_off[EF_MAX_LAYERS];      // offset of W_l^T (l >= 1) inside one ensemble member's T block
+    long long w_off[EF_MAX_LAYERS + 1], b_off[EF_MAX_LAYERS + 1];
+    long long g_off[EF_MAX_LAYERS], be_off[EF_MAX_LAYERS];
+    const float* dout;                    // [nout][ld_o] (+ slot * dout_ss + y * dout_sy)
+    long long dout_ss, dout_sy;
+    int ld_o;
+    const float* U[EF_MAX_LAYERS];        // pre-activations [H][ld_s] (+ slot*s_ss + y*s_sy), column coff + m
+    const float* Ghead;                   // G_{L-1} (head input), same addressing as U
+    const float* MU[EF_MAX_LAYERS];       // LN stats [.] (+ slot*st_ss + y*st_sy), column coff + m
+    const float* RS[EF_MAX_LAYERS];
+    long long s_ss, s_sy, st_ss, st_sy;
+    int ld_s, coff;
+    float* DU[EF_MAX_LAYERS];             // du_l out [H][ld_d] (+ slot*d_ss + y*d_sy)
+    long long d_ss, d_sy;
+    int ld_d;
+    float* part;                          // [slot][y][tile < Mg/16][NP]
+    int NP;
+    int L, M, Mg, nout;
+    int ny, nz;
+    const int* slots;
+};
+bool stream_bwd_supported(int H, int L, int nout, int M, int Mg);
+void launch_stream_bwd(bool ln, const StreamBwdArgs& a, hipStream_t s);
+// Partial index layout of StreamBwdArgs::part (per tile):
+//   [0, L*H) bias of layer l;  LN: [L*H, 2L*H) scale, [2L*H, 3L*H) bias;
+//   then H*nout head kernel W_L[k][j] at k*nout + j.
+inline int stream_bwd_np(int L, int H, int nout, bool ln) { return (ln ? 3 : 1) * L * H + H * nout; }
+
+struct ColsumArgs {                      // grads[off(p)] = sum over tiles of part[t][p]
+    const float* part;
+    int NP, tiles;                        // tiles that hold partials (Mg / 16)
+    float* grads;                         // arena + net offset (slot stride P, ensemble stride ens)
+    long long P, ens;
+    long long b_off[EF_MAX_LAYERS], g_off[EF_MAX_LAYERS], be_off[EF_MAX_LAYERS], w5_off;
+    int L, H, ln;
+    int ny, nz;
+    const int* slots;
+};
+void launch_colsum_reduce(const ColsumArgs& a, hipStream_t s);
+
+// W_l^T copies of the hidden Dense kernels (H x H) for the streamed backward:
+// dst[dst_off[i] + j*H + k] = src[src_off[i] + k*H + j] for every matrix i.
+constexpr int TR_MAX = 32;
+struct TransposeArgs {
+    const float* src;
+    long long src_ss;             // slot stride of src
+    float* dst;
+    long long dst_ss;
+    long long src_off[TR_MAX], dst_off[TR_MAX];
+    int n_mats, H;
+    int nz;
+    const int* slots;             // null: slot = z
+};
+void launch_transpose(const TransposeArgs& a, hipStream_t s);
+
 
 struct BwdArgs {
     TRef dh;              // [H][ld_d] gradient w.r.t. layer output (non-head mode)
@@ -213,6 +282,7 @@ void launch_adam(const AdamArgs& a, hipStream_t s);
 struct FinalArgs {
     const float* stats;           // [slots][n_total_chunks][3]
     const int* chunk_leaf;        // leaf id of every chunk
+    const int* leaf_first;        // [n_leaves + 1]: a leaf's chunks are [leaf_first[l], leaf_first[l+1])
     int n_total_chunks, n_leaves;
     TRef info;
     int* count;

@@ -112,6 +112,14 @@ DEV rsrc_t make_rsrc(const float* p, long long n_elems) {
 DEV float4 bload4(rsrc_t r, int elem_off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, elem_off * 4, 0, 0));
 }
+// dword buffer load / store with a per-lane byte offset and a wave-uniform
+// (SGPR) byte offset: strided per-lane accesses without 64-bit address VGPRs
+DEV float bload1(rsrc_t r, int voff_b, int soff_b) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff_b, soff_b, 0));
+}
+DEV void bstore1(rsrc_t r, float v, int voff_b, int soff_b) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, voff_b, soff_b, 0);
+}
 
 // Global -> register staging of one operand slice.  An "IC" (i-contiguous)
 // operand slice is BK rows (r) x TILE cols (i); an "RC" slice is TILE rows (i)
@@ -530,11 +538,21 @@ void launch_gemm_euler_hidden(const GemmArgs& a, hipStream_t s) {
 // (the padded rows multiply finite parameter words by exact zeros).
 constexpr int EF_H = 512, EF_NC = 16, EF_NW = 8, EF_PF = 8, EF_K0MAX = 64;
 
-// tanh(y) = 1 - 2 / (1 + e^{2y}) on v_exp_f32 (no libm branches)
+// tanh(y) = 1 - 2 / (1 + e^{2y}) on v_exp_f32 (no libm branches; saturates
+// to +-1 correctly for |y| large, absolute error ~1e-7 near 0)
+DEV float tanh_fast(float y) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * y)); }
 DEV float gelu_fast(float x) {
-    const float y = kSqrt2OverPi * (x + 0.044715f * x * x * x);
-    const float t = 1.0f - 2.0f / (1.0f + __expf(2.0f * y));
+    const float t = tanh_fast(kSqrt2OverPi * (x + 0.044715f * x * x * x));
     return 0.5f * x * (1.0f + t);
+}
+DEV void gelu_and_grad_fast(float x, float& g, float& gp) {
+    const float t = tanh_fast(kSqrt2OverPi * (x + 0.044715f * x * x * x));
+    g = 0.5f * x * (1.0f + t);
+    gp = 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * kSqrt2OverPi * (1.0f + 3.0f * 0.044715f * x * x);
+}
+DEV float gelu_grad_fast(float x) {
+    const float t = tanh_fast(kSqrt2OverPi * (x + 0.044715f * x * x * x));
+    return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * kSqrt2OverPi * (1.0f + 3.0f * 0.044715f * x * x);
 }
 
 // One streamed layer's k-loop: acc[c] += W[k][64w + 4li + c] * xs[k][li] over
@@ -1266,6 +1284,312 @@ void launch_input_grad(const InGradArgs& a, hipStream_t s) {
     FQ_KPT_DISPATCH(a.H, FQ_IG_LAUNCH, grid, s, a)
 }
 
+// ==================================================== streamed MLP backward ==
+// jax.grad through the MLP ([EXT] fql/utils/networks.py MLP)
+// of one network in one launch (StreamBwdArgs, kernels.h).  Block = 16 columns
+// x all 512 features of one (member, ensemble member), 8 waves.  Lane (li =
+// lane & 15, lk = lane >> 4) of wave w owns features kq = 64w + 16q + li
+// (q = 0..3) and columns 4lk + r (r = accumulator register), because the dX
+// product is computed TRANSPOSED:
+//   dh^T[m][k] = sum_j du^T[m][j] W_l[k][j]     (v_mfma_f32_16x16x4_f32)
+// with A = du^T from LDS (one ds_read_b128 per k-step of 16 j) and B = rows of
+// W_l streamed from L2 (lane float4 W[kq][16s + 4lk .. +3]: component c feeds
+// MFMA c of k-step s, whose reduction slot lk is j = 16s + 4lk + c).  In this
+// layout the LayerNorm column statistics take one 16-lane DPP row sum and the
+// per-feature sums over the block's columns (parameter grads) two shuffles.
+constexpr int SB_PF = 8;    // float4 W^T loads in flight per lane (as ef_kloop)
+
+template <int CTRL>
+DEV float dpp_mov(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// Sum over the 16 lanes of a DPP row (every lane gets the row's sum):
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror.
+DEV float row16_sum(float v) {
+    v += dpp_mov<0xB1>(v);
+    v += dpp_mov<0x4E>(v);
+    v += dpp_mov<0x141>(v);
+    v += dpp_mov<0x140>(v);
+    return v;
+}
+// Sum over lk (lanes li, li+16, li+32, li+48).
+DEV float lk_sum(float v) {
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    return v;
+}
+
+bool stream_bwd_supported(int H, int L, int nout, int M, int Mg) {
+    return H == EF_H && L >= 1 && L <= EF_MAX_LAYERS && nout >= 1 && nout <= 8 && M % EF_NC == 0 &&
+           Mg % EF_NC == 0 && Mg <= M;
+}
+
+template <bool LN>
+__global__ __launch_bounds__(EF_NW * 64, 1) void stream_bwd_kernel(const StreamBwdArgs g) {
+    constexpr int H = EF_H, NC = EF_NC, NT = EF_NW * 64, PF = SB_PF;
+    __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];  // du_l [H][NC] (+ look-ahead slack)
+    __shared__ float w5s[H * 8];                                      // head kernel W_L [H][nout]
+    __shared__ float colred[2][EF_NW][NC];                            // LN column-stat partials per wave
+    __shared__ float dos[8][NC];                                      // dout of the block's columns
+
+    const int tiles = g.M / NC;
+    const int total = tiles * g.ny * g.nz;
+    const int bid = xcd_remap(blockIdx.x, total);
+    const int tile = bid % tiles, yz = bid / tiles;
+    const int y = yz % g.ny, z = yz / g.ny;
+    const int slot = g.slots[z];
+    const int c0 = tile * NC;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    const int L = g.L, nout = g.nout;
+    const bool gp = c0 < g.Mg;  // the block's columns feed the parameter grads
+    const float* __restrict__ P = g.params + (long long)slot * g.P + (long long)y * g.ens;
+    const float* __restrict__ PTb = g.paramsT + (long long)slot * g.PT + (long long)y * g.ensT;
+    const rsrc_t rT = make_rsrc(PTb, g.ensT);
+    // element offsets of column c0 in the activation / stats / du buffers
+    const long long so = (long long)slot * g.s_ss + (long long)y * g.s_sy + g.coff + c0;
+    const long long sto = (long long)slot * g.st_ss + (long long)y * g.st_sy + g.coff + c0;
+    const long long dso = (long long)slot * g.d_ss + (long long)y * g.d_sy + c0;
+    float* __restrict__ part = gp ? g.part + ((long long)(slot * g.ny + y) * (g.Mg / NC) + tile) * g.NP : nullptr;
+
+    if (tid < nout * NC) {
+        const int j = tid / NC, col = tid % NC;
+        dos[j][col] = g.dout[(long long)slot * g.dout_ss + (long long)y * g.dout_sy + (long long)j * g.ld_o + c0 + col];
+    }
+    for (int e = tid; e < H * nout; e += NT) w5s[e] = P[g.w_off[L] + e];
+    // W^T ring: the first PF k-steps of the first dX product (W_{L-1}^T)
+    const int lo = lk * H + 64 * w + 4 * li;
+    float4 ring[PF];
+    {
+        const int wf = L > 1 ? (int)g.wt_off[L - 1] : 0;
+#pragma unroll
+        for (int p = 0; p < PF; ++p) ring[p] = bload4(rT, wf + 4 * p * H + lo);
+    }
+    __syncthreads();
+
+    // head kernel grad partials (thread = feature): sum_col G_{L-1}[k][col] dout[j][col]
+    if (gp) {
+        const float* __restrict__ gr = g.Ghead + so + (long long)tid * g.ld_s;
+        float gv[NC];
+#pragma unroll
+        for (int q = 0; q < NC / 4; ++q) {
+            const float4 t4 = *reinterpret_cast<const float4*>(gr + 4 * q);
+            gv[4 * q] = t4.x; gv[4 * q + 1] = t4.y; gv[4 * q + 2] = t4.z; gv[4 * q + 3] = t4.w;
+        }
+        const int w5 = (LN ? 3 : 1) * L * H;
+        for (int j = 0; j < nout; ++j) {
+            float v = 0.f;
+#pragma unroll
+            for (int col = 0; col < NC; ++col) v += gv[col] * dos[j][col];
+            part[w5 + tid * nout + j] = v;
+        }
+    }
+    // lane layout (as ef_kloop's accumulators): column li, features f = 64w + 16lk + 4r + c
+    // last hidden layer: dh = W_L dout (nout <= 8, VALU)
+    float dh[4][4];  // [r][c]
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int f = 64 * w + 16 * lk + 4 * r + c;
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < nout) s += w5s[f * nout + j] * dos[j][li];
+            dh[r][c] = s;
+        }
+
+    // epilogue inputs of layer l (u, LN stats, LN scale), loaded one layer ahead
+    // so that their latency hides under the previous dX product
+    float u[4][4], gam[4][4], mu = 0.f, rs = 0.f;
+    auto load_epi = [&](int l) {
+        const rsrc_t rU = make_rsrc(g.U[l] + so, (long long)H * g.ld_s);
+        const int vo = ((64 * w + 16 * lk) * g.ld_s + li) * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) u[r][c] = bload1(rU, vo, (4 * r + c) * g.ld_s * 4);
+        if constexpr (LN) {
+            mu = g.MU[l][sto + li];
+            rs = g.RS[l][sto + li];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float4 g4 = *reinterpret_cast<const float4*>(P + g.g_off[l] + 64 * w + 16 * lk + 4 * r);
+                gam[r][0] = g4.x; gam[r][1] = g4.y; gam[r][2] = g4.z; gam[r][3] = g4.w;
+            }
+        }
+    };
+    load_epi(L - 1);
+    for (int l = L - 1; l >= 0; --l) {
+        // ---- du_l from dh = dL/dG_l: GELU' (and LayerNorm backward) --------
+        float du[4][4];
+        if constexpr (LN) {
+            // pass 1: xhat, GELU' (kept in u), column partials of dh*gamma and dh*gamma*xhat
+            float xh[4][4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    float gv, gpr;
+                    gelu_and_grad_fast(u[r][c], gv, gpr);
+                    u[r][c] = gpr;
+                    xh[r][c] = (gv - mu) * rs;
+                    const float dx = dh[r][c] * gam[r][c];
+                    s1 += dx;
+                    s2 += dx * xh[r][c];
+                }
+            // c1[m] = mean_k(dh gamma), c2[m] = mean_k(dh gamma xhat): lk shuffles, waves via LDS
+            s1 = lk_sum(s1);
+            s2 = lk_sum(s2);
+            if (lk == 0) {
+                colred[0][w][li] = s1;
+                colred[1][w][li] = s2;
+            }
+            __syncthreads();
+            float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+            for (int q8 = 0; q8 < EF_NW; ++q8) {
+                c1 += colred[0][q8][li];
+                c2 += colred[1][q8][li];
+            }
+            c1 = c1 / (float)H;
+            c2 = c2 / (float)H;
+            // pass 2: du = rstd (dh gamma - c1 - xhat c2) gelu'(u); LN grads summed over the 16 columns
+            if (gp) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float sgv[4], sbv[4];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        sgv[c] = row16_sum(dh[r][c] * xh[r][c]);
+                        sbv[c] = row16_sum(dh[r][c]);
+                    }
+                    if (li == 0) {
+                        const int f = 64 * w + 16 * lk + 4 * r;
+                        *reinterpret_cast<float4*>(&part[(L + l) * H + f]) = float4{sgv[0], sgv[1], sgv[2], sgv[3]};
+                        *reinterpret_cast<float4*>(&part[(2 * L + l) * H + f]) = float4{sbv[0], sbv[1], sbv[2], sbv[3]};
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) du[r][c] = rs * (dh[r][c] * gam[r][c] - c1 - xh[r][c] * c2) * u[r][c];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) du[r][c] = dh[r][c] * gelu_grad_fast(u[r][c]);
+        }
+        {
+            const rsrc_t rD = make_rsrc(g.DU[l] + dso, (long long)H * g.ld_d);
+            const int vo = ((64 * w + 16 * lk) * g.ld_d + li) * 4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    bstore1(rD, du[r][c], vo, (4 * r + c) * g.ld_d * 4);
+                    slab[(64 * w + 16 * lk + 4 * r + c) * NC + li] = du[r][c];
+                }
+        }
+        __syncthreads();
+        if (gp) {  // bias grad partial (thread = feature): sum of du over the block's columns
+            const float4* row = reinterpret_cast<const float4*>(&slab[tid * NC]);
+            float sb = 0.f;
+#pragma unroll
+            for (int q = 0; q < NC / 4; ++q) {
+                const float4 t4 = row[q];
+                sb += t4.x + t4.y + t4.z + t4.w;
+            }
+            part[l * H + tid] = sb;
+        }
+        if (l == 0) break;
+
+        // ---- dh_{l-1} = W_l du_l = (W_l^T)^T du_l: the forward k-loop on W_l^T ----
+        load_epi(l - 1);
+        f32x4 acc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int wn = (int)g.wt_off[l >= 2 ? l - 1 : l];  // next product's W^T (l-1 >= 1), else a harmless re-load
+        ef_kloop(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lo, lk, li);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) dh[r][c] = acc[c][r];
+        __syncthreads();  // every wave done with slab / colred
+    }
+}
+
+void launch_stream_bwd(bool ln, const StreamBwdArgs& a, hipStream_t s) {
+    const dim3 grid((a.M / EF_NC) * a.ny * a.nz), block(EF_NW * 64);
+    if (ln) hipLaunchKernelGGL((stream_bwd_kernel<true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((stream_bwd_kernel<false>), grid, block, 0, s, a);
+}
+
+// Fold the per-tile partials of stream_bwd into the grads (fixed tile order:
+// deterministic).  Index layout: stream_bwd_np (kernels.h).
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const ColsumArgs a) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y, z = blockIdx.z;
+    if (p >= a.NP) return;
+    const int slot = a.slots[z];
+    const float* __restrict__ src = a.part + (long long)(slot * a.ny + y) * a.tiles * a.NP + p;
+    float s = 0.f;
+    for (int t = 0; t < a.tiles; ++t) s += src[(long long)t * a.NP];
+    const int LH = a.L * a.H;
+    const int reg = p < LH ? 0 : !a.ln ? 3 : p < 2 * LH ? 1 : p < 3 * LH ? 2 : 3;
+    const int pr = reg == 3 ? p - (a.ln ? 3 : 1) * LH : p - reg * LH;
+    long long off = a.w5_off + pr;
+    if (reg < 3) {
+        const int l = pr / a.H, k = pr % a.H;
+#pragma unroll
+        for (int i = 0; i < EF_MAX_LAYERS; ++i)
+            if (i == l) off = (reg == 0 ? a.b_off[i] : reg == 1 ? a.g_off[i] : a.be_off[i]) + k;
+    }
+    a.grads[(long long)slot * a.P + (long long)y * a.ens + off] = s;
+}
+
+void launch_colsum_reduce(const ColsumArgs& a, hipStream_t s) {
+    const dim3 grid((a.NP + 255) / 256, a.ny, a.nz);
+    hipLaunchKernelGGL(colsum_reduce_kernel, grid, dim3(256), 0, s, a);
+}
+
+// W^T copies of the hidden kernels (64 x 64 tiles through LDS).
+__global__ __launch_bounds__(256) void transpose_kernel(const TransposeArgs a) {
+    __shared__ float t[64][65];
+    const int H = a.H, tpr = H / 64;
+    const int tr = blockIdx.x / tpr, tc = blockIdx.x % tpr;  // source tile rows k, cols j
+    const int mi = blockIdx.y, z = blockIdx.z;
+    const int slot = a.slots ? a.slots[z] : z;
+    long long so = 0, dof = 0;
+#pragma unroll
+    for (int i = 0; i < TR_MAX; ++i)
+        if (i == mi) { so = a.src_off[i]; dof = a.dst_off[i]; }
+    const float* __restrict__ src = a.src + (long long)slot * a.src_ss + so;
+    float* __restrict__ dst = a.dst + (long long)slot * a.dst_ss + dof;
+    const int k0 = tr * 64, j0 = tc * 64;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int idx = threadIdx.x + 256 * p, r = idx / 16, c4 = idx % 16;
+        const float4 v = *reinterpret_cast<const float4*>(src + (long long)(k0 + r) * H + j0 + 4 * c4);
+        t[r][4 * c4] = v.x; t[r][4 * c4 + 1] = v.y; t[r][4 * c4 + 2] = v.z; t[r][4 * c4 + 3] = v.w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int idx = threadIdx.x + 256 * p, r = idx / 16, c4 = idx % 16;  // dst row j0 + r, cols k0 + 4c4..
+        *reinterpret_cast<float4*>(dst + (long long)(j0 + r) * H + k0 + 4 * c4) =
+            float4{t[4 * c4][r], t[4 * c4 + 1][r], t[4 * c4 + 2][r], t[4 * c4 + 3][r]};
+    }
+}
+
+void launch_transpose(const TransposeArgs& a, hipStream_t s) {
+    if (a.n_mats == 0 || a.nz == 0) return;
+    const dim3 grid((a.H / 64) * (a.H / 64), a.n_mats, a.nz);
+    hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, s, a);
+}
+
 // =============================================================== RNG =======
 // Philox4x32-10 (Salmon et al. 2011), counter = (row, step, salt, word).
 DEV void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
@@ -1301,69 +1625,51 @@ DEV void philox_normals(float* n, int cnt, uint64_t seed, uint32_t row, uint32_t
 // draws + assembly of every network's first-layer input (feature-major
 // concatenation = stacking row blocks).  Injected mode reads batch/noise from
 // a packed staging buffer instead (parity tests).
+// Thread = (minibatch row b, part p of SP): every part draws the row index and
+// t (Philox word 0), then part p writes the features k = p mod SP, the Philox
+// normal pairs q = p mod SP and action j = p.  Values are identical to a
+// one-thread-per-row draw (same counters).
+constexpr int SP = 8;
 __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
-    const int nbb = (a.B + 255) / 256;
+    constexpr int RPB = 256 / SP;  // rows per block
+    const int nbb = (a.B + RPB - 1) / RPB;
     const int bb = blockIdx.x % nbb, z = blockIdx.x / nbb;
     const int slot = a.slots[z];
-    const int b = bb * 256 + threadIdx.x;
+    const int b = bb * RPB + (int)(threadIdx.x / SP), p = threadIdx.x % SP;
     if (b >= a.B) return;
     const int B = a.B, D = a.D, A = a.A;
-    float zn[8], x0[8], zd[8], zm[8], act[8];
-    float t, rew, mask;
-    const float *obs, *nobs;
     const uint64_t seed = a.seeds[slot];
     const uint32_t step = (uint32_t)a.count[slot];
-    // minibatch: injected (packed per active member) or drawn from the dataset
-    if (a.inj_batch) {
-        const long long bs = (long long)B * (2 * D + A + 2);
-        const float* pb = a.inj_batch + z * bs;
-        obs = pb + (long long)b * D;
-        const float* pa = pb + (long long)B * D;
-        rew = pb[(long long)B * (D + A) + b];
-        mask = pb[(long long)B * (D + A + 1) + b];
-        nobs = pb + (long long)B * (D + A + 2) + (long long)b * D;
-        for (int j = 0; j < A; ++j) act[j] = pa[b * A + j];
-    } else {
-        uint32_t c[4] = {(uint32_t)b, step, a.stream_salt, 0u};
-        philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-        const long long idx = (long long)(((unsigned long long)c[0] * (unsigned long long)a.n_rows) >> 32);
-        for (int j = 0; j < A; ++j) act[j] = a.act[idx * A + j];
-        obs = a.obs + idx * D;
-        nobs = a.nobs + idx * D;
-        rew = a.rew[idx];
-        mask = a.mask[idx];
-    }
-    // noise: injected or drawn on device (Philox keyed by member seed, update count)
-    if (a.inj_noise) {
-        const long long ns = (long long)B * (4 * A + 1);
-        const float* pn = a.inj_noise + z * ns;
-        for (int j = 0; j < A; ++j) {
-            zn[j] = pn[b * A + j];
-            x0[j] = pn[(long long)B * A + b * A + j];
-            zd[j] = pn[(long long)B * (2 * A + 1) + b * A + j];
-            zm[j] = pn[(long long)B * (3 * A + 1) + b * A + j];
-        }
-        t = pn[(long long)B * 2 * A + b];
-    } else {
-        uint32_t c[4] = {(uint32_t)b, step, a.stream_salt, 0u};
-        philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-        t = u01(c[1]);
-        float nrm[32];
-        philox_normals(nrm, 4 * A, seed, (uint32_t)b, step, a.stream_salt);
-        for (int j = 0; j < A; ++j) {
-            zn[j] = nrm[j];
-            x0[j] = nrm[A + j];
-            zd[j] = nrm[2 * A + j];
-            zm[j] = nrm[3 * A + j];
-        }
-    }
+    const long long B2 = 2 * (long long)B, B3 = 3 * (long long)B;
     float* os = at(a.os_in, slot);
     float* bc = at(a.bc_in, slot);
     float* cr = at(a.cr_in, slot);
     float* tg = at(a.tg_in, slot);
     float* eu = at(a.eu_in, slot);
-    const long long B2 = 2 * (long long)B, B3 = 3 * (long long)B;
-    for (int k = 0; k < D; ++k) {
+    uint32_t c0[4] = {(uint32_t)b, step, a.stream_salt, 0u};
+    philox4x32_10(c0, (uint32_t)seed, (uint32_t)(seed >> 32));
+    // minibatch row: injected (packed per active member) or drawn from the dataset
+    const float *obs, *nobs, *actp;
+    float rew, mask;
+    if (a.inj_batch) {
+        const long long bs = (long long)B * (2 * D + A + 2);
+        const float* pb = a.inj_batch + z * bs;
+        obs = pb + (long long)b * D;
+        actp = pb + (long long)B * D + (long long)b * A;
+        rew = pb[(long long)B * (D + A) + b];
+        mask = pb[(long long)B * (D + A + 1) + b];
+        nobs = pb + (long long)B * (D + A + 2) + (long long)b * D;
+    } else {
+        const long long idx = (long long)(((unsigned long long)c0[0] * (unsigned long long)a.n_rows) >> 32);
+        actp = a.act + idx * A;
+        obs = a.obs + idx * D;
+        nobs = a.nobs + idx * D;
+        rew = a.rew[idx];
+        mask = a.mask[idx];
+    }
+    const float* pn = a.inj_noise ? a.inj_noise + z * (long long)B * (4 * A + 1) : nullptr;
+    const float t = pn ? pn[(long long)B * 2 * A + b] : u01(c0[1]);
+    for (int k = p; k < D; k += SP) {
         const float o = obs[k], n = nobs[k];
         os[k * B3 + b] = n;
         os[k * B3 + B + b] = o;
@@ -1375,27 +1681,62 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
         tg[(long long)k * B + b] = n;
         eu[(long long)k * B + b] = o;
     }
-    float* at_ = at(a.act_t, slot);
-    float* x0_ = at(a.x0_t, slot);
-    for (int j = 0; j < A; ++j) {
-        const long long r = D + j;
-        os[r * B3 + b] = zn[j];
-        os[r * B3 + B + b] = zd[j];
-        os[r * B3 + 2 * B + b] = zm[j];
-        bc[r * B2 + b] = (1.0f - t) * x0[j] + t * act[j];
-        bc[r * B2 + B + b] = zd[j];
-        cr[r * B2 + b] = act[j];
-        at_[(long long)j * B + b] = act[j];
-        x0_[(long long)j * B + b] = x0[j];
+    if (p < A) {
+        const float av = actp[p];
+        cr[(D + p) * B2 + b] = av;
+        at(a.act_t, slot)[(long long)p * B + b] = av;
     }
-    bc[(long long)(D + A) * B2 + b] = t;
-    bc[(long long)(D + A) * B2 + B + b] = 0.0f;
-    at(a.rew_t, slot)[b] = rew;
-    at(a.mask_t, slot)[b] = mask;
+    // noises: normal i of 4A -> (category i / A: z_next, x0, z_d, z_metric; action j = i % A)
+    for (int q = p; 2 * q < 4 * A; q += SP) {
+        float nv[2];
+        if (pn) {
+            for (int h = 0; h < 2; ++h) {
+                const int i = 2 * q + h, cat = i / A, j = i % A;
+                const long long o = cat == 0 ? (long long)b * A + j
+                                  : cat == 1 ? (long long)B * A + b * A + j
+                                  : cat == 2 ? (long long)B * (2 * A + 1) + b * A + j
+                                             : (long long)B * (3 * A + 1) + b * A + j;
+                nv[h] = i < 4 * A ? pn[o] : 0.f;
+            }
+        } else {
+            uint32_t c[4] = {(uint32_t)b, step, a.stream_salt, 1u + (uint32_t)q};
+            philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+            const float r = sqrtf(-2.0f * logf(u01_open_closed(c[0])));
+            float sv, cv;
+            sincosf(6.283185307179586f * u01(c[1]), &sv, &cv);
+            nv[0] = r * cv;
+            nv[1] = r * sv;
+        }
+        for (int h = 0; h < 2; ++h) {
+            const int i = 2 * q + h;
+            if (i >= 4 * A) break;
+            const int cat = i / A, j = i % A;
+            const long long r = D + j;
+            const float v = nv[h];
+            if (cat == 0) {
+                os[r * B3 + b] = v;
+            } else if (cat == 1) {
+                at(a.x0_t, slot)[(long long)j * B + b] = v;
+                bc[r * B2 + b] = (1.0f - t) * v + t * actp[j];
+            } else if (cat == 2) {
+                os[r * B3 + B + b] = v;
+                bc[r * B2 + B + b] = v;
+            } else {
+                os[r * B3 + 2 * B + b] = v;
+            }
+        }
+    }
+    if (p == 0) {
+        bc[(long long)(D + A) * B2 + b] = t;
+        bc[(long long)(D + A) * B2 + B + b] = 0.0f;
+        at(a.rew_t, slot)[b] = rew;
+        at(a.mask_t, slot)[b] = mask;
+    }
 }
 
 void launch_sample(const SampleArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(sample_kernel, dim3(((a.B + 255) / 256) * a.nz), dim3(256), 0, s, a);
+    const int rpb = 256 / SP;
+    hipLaunchKernelGGL(sample_kernel, dim3(((a.B + rpb - 1) / rpb) * a.nz), dim3(256), 0, s, a);
 }
 
 // =============================================================== losses ====
@@ -1641,32 +1982,43 @@ void launch_adam(const AdamArgs& a, hipStream_t s) {
 }
 
 // grad/max, grad/min over every leaf (target-critic leaves contribute zeros),
-// grad/norm = sum over leaves of the leaf L2 norm; count += 1.
-__global__ __launch_bounds__(64) void finalize_kernel(const FinalArgs a) {
+// grad/norm = sum over leaves of the leaf L2 norm; count += 1.  Thread = leaf
+// (its chunks in order), then fixed-pattern reductions: deterministic.
+__global__ __launch_bounds__(128) void finalize_kernel(const FinalArgs a) {
     const int z = blockIdx.x, slot = a.slots[z];
-    __shared__ float leaf_ss[128];
-    for (int i = threadIdx.x; i < 128; i += 64) leaf_ss[i] = 0.f;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const float* st = a.stats + (long long)slot * a.n_total_chunks * 3;
-        float mx = 0.f, mn = 0.f;  // zero target-critic leaves are part of the tree
-        for (int c = 0; c < a.n_total_chunks; ++c) {
+    const int t = threadIdx.x;
+    const float* st = a.stats + (long long)slot * a.n_total_chunks * 3;
+    float mx = 0.f, mn = 0.f, nrm = 0.f;  // zero target-critic leaves are part of the tree
+    if (t < a.n_leaves) {
+        float ss = 0.f;
+        for (int c = a.leaf_first[t]; c < a.leaf_first[t + 1]; ++c) {
             mx = fmaxf(mx, st[c * 3 + 0]);
             mn = fminf(mn, st[c * 3 + 1]);
-            leaf_ss[a.chunk_leaf[c]] += st[c * 3 + 2];
+            ss += st[c * 3 + 2];
         }
-        float nrm = 0.f;
-        for (int l = 0; l < a.n_leaves; ++l) nrm += sqrtf(leaf_ss[l]);
+        nrm = sqrtf(ss);
+    }
+    __shared__ float red[3][2];
+    mx = wave_max(mx);
+    mn = wave_min(mn);
+    nrm = wave_sum(nrm);
+    if ((t & 63) == 0) {
+        red[0][t >> 6] = mx;
+        red[1][t >> 6] = mn;
+        red[2][t >> 6] = nrm;
+    }
+    __syncthreads();
+    if (t == 0) {
         float* info = at(a.info, slot);
-        info[10] = mx;
-        info[11] = mn;
-        info[12] = nrm;
+        info[10] = fmaxf(red[0][0], red[0][1]);
+        info[11] = fminf(red[1][0], red[1][1]);
+        info[12] = red[2][0] + red[2][1];
         a.count[slot] += 1;
     }
 }
 
 void launch_finalize(const FinalArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(a.nz), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(finalize_kernel, dim3(a.nz), dim3(128), 0, s, a);
 }
 
 // ================================================================= init ====

@@ -131,6 +131,7 @@ struct fqlpop {
     float* stats = nullptr;
     Chunk* chunks = nullptr;
     int* chunk_leaf = nullptr;
+    int* leaf_first = nullptr;
     int n_chunks_net[3] = {0, 0, 0}, chunk_base_net[3] = {0, 0, 0}, n_chunks_total = 0;
     int n_train_leaves = 0;
 
@@ -167,6 +168,13 @@ struct fqlpop {
     // used by alternate steps so the host reads step i-2 while step i runs
     bool euler_fused = false;      // Euler steps 1..S-1 as one persistent launch (euler_flow_kernel)
     bool stream_fwd = false;       // whole-network forward launches (stream_fwd_kernel)
+    bool stream_bwd = false;       // whole-network dX chains (stream_bwd_kernel)
+    float *part_cr = nullptr, *part_bc = nullptr, *part_os = nullptr;  // stream_bwd column-sum partials
+    // W_l^T copies of the hidden kernels (l = 1..L-1) for stream_bwd, per slot:
+    // [critic e=0..E-1 | bc | os] x (L-1) x H x H; refreshed after each Adam
+    float* paramsT = nullptr;
+    long long PTT = 0, wt_net_off[3] = {0, 0, 0};
+    bool wt_dirty = true;          // params changed on the host side: re-transpose before the next step
     bool probe = false;
     int probe_set = -1;            // set used by the step being enqueued (-1: none)
     int probe_idx = 0;             // next launch slot of that set
@@ -287,6 +295,13 @@ void build_chunks(fqlpop* h) {
     ARGCHK(leaf_id <= 128, "too many leaves");
     HIPCHK(hipMalloc(&h->chunks, sizeof(Chunk) * all.size()));
     HIPCHK(hipMemcpy(h->chunks, all.data(), sizeof(Chunk) * all.size(), hipMemcpyHostToDevice));
+    std::vector<int> first(leaf_id + 1, 0);
+    for (size_t c = all_leaf.size(); c-- > 0;) first[all_leaf[c]] = (int)c;
+    first[leaf_id] = (int)all_leaf.size();
+    for (size_t c = 1; c < all_leaf.size(); ++c)
+        ARGCHK(all_leaf[c] >= all_leaf[c - 1], "chunks of a leaf must be contiguous");
+    HIPCHK(hipMalloc(&h->leaf_first, sizeof(int) * first.size()));
+    HIPCHK(hipMemcpy(h->leaf_first, first.data(), sizeof(int) * first.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMalloc(&h->chunk_leaf, sizeof(int) * all_leaf.size()));
     HIPCHK(hipMemcpy(h->chunk_leaf, all_leaf.data(), sizeof(int) * all_leaf.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMalloc(&h->stats, sizeof(float) * 3 * all.size() * h->n));
@@ -324,6 +339,7 @@ void init_member(fqlpop* h, int slot, uint64_t seed) {
                           sizeof(float) * h->PT, hipMemcpyDeviceToDevice, h->sM));
     HIPCHK(hipMemsetAsync(h->count + slot, 0, sizeof(int), h->sM));
     HIPCHK(hipStreamSynchronize(h->sM));
+    h->wt_dirty = true;
 }
 
 // ------------------------------------------------------------- DAG helpers
@@ -492,6 +508,105 @@ void bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_
             gemm(LAYOUT_DX, EPI_STORE, gx, s);
         }
     }
+}
+
+// Whole-network backward of `N` (stream_bwd_kernel) on `s`: dX chain from the
+// head gradient `dout` ([nout][ld_o]) down to du_0, LayerNorm / GELU' fused,
+// parameter-grad column sums as per-tile partials.  Then, on `sw`, the
+// partial reduction (bias / LN / head-kernel grads) and the dW_l GEMMs.
+// Activations are read at column offset `coff` (ld `ld`), du_l written with
+// ld `ld_d`; M columns are back-propagated, the first Mg feed the grads.
+void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_o, TRef X0, int ld,
+                    long long coff, int M, int Mg, const std::vector<float*>& U, const std::vector<float*>& G,
+                    long long act_sy, const std::vector<float*>* MU, const std::vector<float*>* RS, long long st_sy,
+                    const std::vector<float*>& DU, int ld_d, float* part, hipStream_t sw) {
+    fqlpop* h = c.h;
+    const long long act_ss = (long long)N.H * ld * N.E;
+    const long long d_ss = (long long)N.H * ld_d * N.E, d_sy = (long long)N.H * ld_d;
+    StreamBwdArgs a{};
+    a.params = h->params + N.off;
+    a.P = h->P; a.ens = N.ens_size;
+    const int ni = &N == &h->critic ? 0 : &N == &h->bc ? 1 : 2;
+    a.paramsT = h->paramsT + h->wt_net_off[ni];
+    a.PT = h->PTT; a.ensT = (long long)(N.L - 1) * N.H * N.H;
+    for (int l = 1; l < N.L; ++l) a.wt_off[l] = (long long)(l - 1) * N.H * N.H;
+    for (int l = 0; l <= N.L; ++l) {
+        a.w_off[l] = N.W[l];
+        a.b_off[l] = N.b[l];
+        if (l < N.L) {
+            if (N.ln) {
+                a.g_off[l] = N.gam[l];
+                a.be_off[l] = N.bet[l];
+                a.MU[l] = (*MU)[l];
+                a.RS[l] = (*RS)[l];
+            }
+            a.U[l] = U[l];
+            a.DU[l] = DU[l];
+        }
+    }
+    a.dout = dout.p; a.dout_ss = dout.ss; a.dout_sy = dout.sy; a.ld_o = ld_o;
+    a.Ghead = G[N.L - 1];
+    a.s_ss = act_ss; a.s_sy = act_sy; a.st_ss = (long long)ld * N.E; a.st_sy = st_sy;
+    a.ld_s = ld; a.coff = (int)coff;
+    a.d_ss = d_ss; a.d_sy = d_sy; a.ld_d = ld_d;
+    a.part = part; a.NP = stream_bwd_np(N.L, N.H, N.out_dim, N.ln);
+    a.L = N.L; a.M = M; a.Mg = Mg; a.nout = N.out_dim;
+    a.ny = N.E; a.nz = c.nz; a.slots = h->slots;
+    launch_stream_bwd(N.ln, a, s);
+    if (sw != s) {
+        hipEvent_t ev = next_event(h);
+        HIPCHK(hipEventRecord(ev, s));
+        HIPCHK(hipStreamWaitEvent(sw, ev, 0));
+    }
+    ColsumArgs r{};
+    r.part = part; r.NP = a.NP; r.tiles = Mg / 16;
+    r.grads = h->grads + N.off; r.P = h->P; r.ens = N.ens_size;
+    for (int l = 0; l < N.L; ++l) {
+        r.b_off[l] = N.b[l];
+        if (N.ln) { r.g_off[l] = N.gam[l]; r.be_off[l] = N.bet[l]; }
+    }
+    r.w5_off = N.W[N.L];
+    r.L = N.L; r.H = N.H; r.ln = N.ln ? 1 : 0;
+    r.ny = N.E; r.nz = c.nz; r.slots = h->slots;
+    launch_colsum_reduce(r, sw);
+    auto act = [&](float* p) { return tref(p + coff, act_ss, act_sy); };
+    for (int l = N.L - 1; l >= 0; --l) {
+        GemmArgs gw{};
+        gw.A = l == 0 ? X0 : act(G[l - 1]);
+        gw.B = tref(DU[l], d_ss, d_sy);
+        gw.C = pref(h, h->grads, N, N.W[l]);
+        gw.M = N.kdim(l); gw.N = N.H; gw.K = Mg;
+        gw.lda = ld; gw.ldb = ld_d; gw.ldc = N.H;
+        gw.ny = N.E; gw.nz = c.nz; gw.slots = h->slots;
+        gemm(LAYOUT_DW, EPI_STORE, gw, sw);
+    }
+}
+
+// Refresh the W^T copies of the nets in `mask` (bit ni: 0 critic, 1 bc, 2 os)
+// for the active slots (all slots when all_slots).
+void transpose_nets(fqlpop* h, hipStream_t s, int mask, bool all_slots) {
+    TransposeArgs t{};
+    t.src = h->params; t.src_ss = h->P;
+    t.dst = h->paramsT; t.dst_ss = h->PTT;
+    t.H = h->H;
+    const NetLayout* nets[3] = {&h->critic, &h->bc, &h->os};
+    const long long HH = (long long)h->H * h->H;
+    int n = 0;
+    for (int ni = 0; ni < 3; ++ni) {
+        if (!(mask & (1 << ni))) continue;
+        const NetLayout& N = *nets[ni];
+        for (int e = 0; e < N.E; ++e)
+            for (int l = 1; l < N.L; ++l) {
+                ARGCHK(n < TR_MAX, "too many transposed matrices");
+                t.src_off[n] = N.off + e * N.ens_size + N.W[l];
+                t.dst_off[n] = h->wt_net_off[ni] + ((long long)e * (N.L - 1) + (l - 1)) * HH;
+                ++n;
+            }
+    }
+    t.n_mats = n;
+    if (all_slots) { t.slots = nullptr; t.nz = h->n; }
+    else { t.slots = h->slots; t.nz = h->nz; }
+    launch_transpose(t, s);
 }
 
 void adam_net(const Ctx& c, hipStream_t s, int ni) {
@@ -692,10 +807,15 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     HIPCHK(hipEventRecord(h->ev_bcloss, sB));
     if (train) {
         const NetLayout& N = h->bc;
-        bwd_net(c, sB, N, tref(h->dv, (long long)A * B), B, tref(h->bc_in, (long long)Kb * B2), B2, 0, B, B,
-                h->bc_u, h->bc_g, 0, nullptr, nullptr, 0, h->bc_du, h->bc_dh, nullptr, nullptr, B, sB);
+        if (h->stream_bwd)
+            stream_bwd_net(c, sB, N, tref(h->dv, (long long)A * B), B, tref(h->bc_in, (long long)Kb * B2), B2, 0, B,
+                           B, h->bc_u, h->bc_g, 0, nullptr, nullptr, 0, h->bc_du, B, h->part_bc, sB);
+        else
+            bwd_net(c, sB, N, tref(h->dv, (long long)A * B), B, tref(h->bc_in, (long long)Kb * B2), B2, 0, B, B,
+                    h->bc_u, h->bc_g, 0, nullptr, nullptr, 0, h->bc_du, h->bc_dh, nullptr, nullptr, B, sB);
         HIPCHK(hipStreamWaitEvent(sB, h->ev_flow, 0));  // Euler reads bc params
         adam_net(c, sB, 1);
+        if (h->stream_bwd) transpose_nets(h, sB, 2, false);
     }
     HIPCHK(hipEventRecord(h->ev_bdone, sB));
 
@@ -779,9 +899,13 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     launch_loss_critic(la, sM);
     if (train) {
         // critic backward: the dX chain stays on sM, the dW GEMMs go to sX
-        bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0), B2, 0,
-                B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, h->cr_dh, h->cr_c1, h->cr_c2, B2,
-                sX);
+        if (h->stream_bwd)
+            stream_bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0),
+                           B2, 0, B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, B2, h->part_cr, sX);
+        else
+            bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0), B2, 0,
+                    B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, h->cr_dh, h->cr_c1, h->cr_c2,
+                    B2, sX);
         InGradArgs ig{};
         ig.W0 = pref(h, h->params, NC, NC.W[0]);
         ig.du0 = tref(h->cr_du[0], (long long)H * B2 * E, sy2);
@@ -792,20 +916,26 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         // critic Adam + target EMA once every read of the critic params is done
         dep(sM, sX);
         adam_net(c, sX, 0);
+        if (h->stream_bwd) transpose_nets(h, sX, 1, false);
     }
     HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
     HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
     launch_loss_actor(la, sM);
     if (train) {
         const NetLayout& N = h->os;
-        bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3, B, B, B,
-                h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, h->os_dh, nullptr, nullptr, B, sX);
+        if (h->stream_bwd)
+            stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3,
+                           B, B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, B, h->part_os, sX);
+        else
+            bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3, B, B,
+                    B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, h->os_dh, nullptr, nullptr, B, sX);
         dep(sM, sX);
         adam_net(c, sX, 2);
+        if (h->stream_bwd) transpose_nets(h, sX, 4, false);
         dep(sX, sM);
         HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
         FinalArgs fa{};
-        fa.stats = h->stats; fa.chunk_leaf = h->chunk_leaf;
+        fa.stats = h->stats; fa.chunk_leaf = h->chunk_leaf; fa.leaf_first = h->leaf_first;
         fa.n_total_chunks = h->n_chunks_total; fa.n_leaves = h->n_train_leaves;
         fa.info = tref(h->info, FQLPOP_INFO_STRIDE);
         fa.count = h->count;
@@ -819,6 +949,10 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
 
 void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     if (h->nz == 0) return;
+    if (train && h->stream_bwd && h->wt_dirty) {  // params set on the host side since the last step
+        transpose_nets(h, h->sM, 7, true);
+        h->wt_dirty = false;
+    }
     if (!h->cfg.use_graph) {
         enqueue(h, train, inj_batch, inj_noise);
         return;
@@ -1001,6 +1135,11 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             const char* sf = std::getenv("FQLPOP_STREAM");
             h->stream_fwd = stream_fwd_supported(H, L, D + A + 1, A, B) && !(sf && std::atoi(sf) == 0);
         }
+        {
+            const char* sb = std::getenv("FQLPOP_SBWD");
+            h->stream_bwd = stream_bwd_supported(H, L, A, B, B) &&
+                            !(sb && std::atoi(sb) == 0);
+        }
         if (h->euler_fused) {  // dominant kernel: one persistent Euler launch per step
             h->probe_pairs = 1;
             h->probe_blocks = (long long)(cfg->batch_size / 16) * n_members;
@@ -1056,6 +1195,18 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             h->bc_du.push_back(h->alloc((long long)H * B));
             h->os_du.push_back(h->alloc((long long)H * B));
         }
+        if (h->stream_bwd) {
+            const int T = B / 16;  // tiles with partials (Mg = B for every net)
+            h->part_cr = h->alloc((long long)E * T * stream_bwd_np(L, H, 1, h->critic.ln));
+            h->part_bc = h->alloc((long long)T * stream_bwd_np(L, H, A, h->bc.ln));
+            h->part_os = h->alloc((long long)T * stream_bwd_np(L, H, A, h->os.ln));
+            const long long HH = (long long)H * H;
+            h->wt_net_off[0] = 0;
+            h->wt_net_off[1] = (long long)E * (L - 1) * HH;
+            h->wt_net_off[2] = (long long)(E + 1) * (L - 1) * HH;
+            h->PTT = (long long)(E + 2) * (L - 1) * HH;
+            h->paramsT = h->alloc(std::max<long long>(1, h->PTT));
+        }
         h->cr_dh = h->alloc((long long)H * B2 * E);
         h->bc_dh = h->alloc((long long)H * B);
         h->os_dh = h->alloc((long long)H * B);
@@ -1098,7 +1249,7 @@ int fqlpop_destroy(fqlpop_t* h) {
         for (float* p : h->allocs) (void)hipFree(p);
         for (void* p : {(void*)h->params, (void*)h->grads, (void*)h->adam_m, (void*)h->adam_v, (void*)h->target,
                         (void*)h->count, (void*)h->seeds, (void*)h->alpha, (void*)h->slots, (void*)h->stats,
-                        (void*)h->chunks, (void*)h->chunk_leaf})
+                        (void*)h->chunks, (void*)h->chunk_leaf, (void*)h->leaf_first})
             if (p) (void)hipFree(p);
         for (auto& d : h->ds)
             for (float* p : {d.obs, d.act, d.rew, d.mask, d.nobs})
@@ -1327,6 +1478,7 @@ static void state_copy(fqlpop* h, int member, int which, float* flat, const floa
         }
     }
     if (!get) {
+        if (which == 0) h->wt_dirty = true;
         HIPCHK(hipMemcpy(arena + (long long)member * h->P, blk.data(), sizeof(float) * h->P, hipMemcpyHostToDevice));
         if (which == 0)
             HIPCHK(hipMemcpy(h->target + (long long)member * h->PT, tblk.data(), sizeof(float) * h->PT,

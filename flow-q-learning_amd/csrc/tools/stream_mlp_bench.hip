@@ -434,6 +434,9 @@ int main(int argc, char** argv) {
     std::vector<float> ref(nX);
     CK(hipMemcpy(ref.data(), in, 4 * nX, hipMemcpyDeviceToHost));
     run_cg<8, 1, 0>(nm, iters, W, b, X, Y, ref, ncols, s);
+    run_cg<8, 1, 1>(nm, iters, W, b, X, Y, ref, ncols, s);
+    run_cg<8, 1, 2>(nm, iters, W, b, X, Y, ref, ncols, s);
+    run_cg<8, 2, 0>(nm, iters, W, b, X, Y, ref, ncols, s);
     run_dx<2>(nm, iters, W, b, X, Y, T0, T1, ncols, s);
     run_dx<4>(nm, iters, W, b, X, Y, T0, T1, ncols, s);
     return 0;
