@@ -97,6 +97,39 @@ def cpu_baseline(wl: dict, data: dict, budget_s: float, threads: int) -> dict:
                       f"float32 PyTorch-CPU restatement (oracle/fql_torch.py), torch threads={threads}"}
 
 
+def eval_rollout_leg(pop, wl: dict, n_envs: int, steps: int, dev) -> dict:
+    """World-model evaluation of every member (BASELINE config 5's eval; SURVEY.md
+    8f rank 1): one fqlpop_rollout launch, 512-wide actor + BaselineStatePredictor
+    (128, 256, 128) + TerminationPredictor (128, 256, 128), synthetic env model
+    whose termination logit stays negative so every episode runs `steps` steps.
+    Outside the timed region; reported beside the headline, not in `value`."""
+    import envmodel as em
+    D, A = wl["obs_dim"], wl["action_dim"]
+    spec = em.EnvModelSpec(D, A)
+    sp = em.init_state_predictor(spec, 0, scale=0.1)
+    tp = em.init_termination_predictor(spec, 1, scale=0.0, bias=-1.0)
+    pop.set_env_model(em.flatten_state_predictor(spec, sp), em.flatten_termination_predictor(spec, tp),
+                      spec.sp_hidden, spec.tp_hidden)
+    obs0 = np.random.default_rng(0).standard_normal((n_envs, D)).astype(np.float32)
+    pop.rollout(obs0, 2, seed=1)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    succ, length = pop.rollout(obs0, steps, seed=2)
+    el = time.perf_counter() - t0
+    H = 512
+    f_actor = 2.0 * ((D + A) * H + 3 * H * H + H * A)
+    sd, td = spec.sp_dims(), spec.tp_dims()
+    f_env = 2.0 * sum(sd[i] * sd[i + 1] for i in range(len(sd) - 1)) + 2.0 * sum(
+        td[i] * td[i + 1] for i in range(len(td) - 1))
+    env_steps = float(length.sum())
+    return {"members": int(succ.shape[0]), "envs_per_member": n_envs, "max_episode_steps": steps,
+            "ms": round(1000.0 * el, 3), "env_steps_per_s": round(env_steps / el, 1),
+            "tflops": round(env_steps * (f_actor + f_env) / el / 1e12, 3),
+            "episodes_all_full_length": bool(np.all(length == steps)),
+            "note": "one launch, 16 envs per block, all steps on device (sample_actions + state predictor + "
+                    "termination predictor); host-synchronised wall time incl. H2D of init obs"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,6 +147,9 @@ def main():
                          "(csrc/tools/pmc_summary.py output); missing file -> traffic null")
     ap.add_argument("--no-probe", action="store_true",
                     help="time the step without the in-step timing nodes of the dominant kernel")
+    ap.add_argument("--eval-envs", type=int, default=50, help="world-model rollout leg: envs per member "
+                    "(reference eval_episodes); 0 disables the leg")
+    ap.add_argument("--eval-steps", type=int, default=1000, help="world-model rollout leg: max_episode_steps")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -237,6 +273,8 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if args.eval_envs > 0:
+        result["eval_rollout"] = eval_rollout_leg(pop, wl, args.eval_envs, args.eval_steps, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
         log(f"[rank 0] cpu baseline ({args.cpu_baseline_seconds:.0f} s budget, {threads} threads)")

@@ -48,6 +48,15 @@ void launch_gemm(int layout, int epi, int tile, const GemmArgs& a, hipStream_t s
 void launch_gemm_euler_hidden(const GemmArgs& a, hipStream_t s);
 // variant: bit 0 = K slice 64 (else 32), bit 1 = two accumulator chains
 void launch_gemm_variant(int layout, int epi, int tile, int variant, const GemmArgs& a, hipStream_t s);
+// Up to GEMM_GROUP_MAX independent dW-layout problems (A and B both
+// r-contiguous, EPI_STORE) in one launch; N % BN == 0 for every problem.
+constexpr int GEMM_GROUP_MAX = 8;
+struct GemmGroupArgs {
+    GemmArgs g[GEMM_GROUP_MAX];
+    int first[GEMM_GROUP_MAX + 1];   // prefix of per-problem block counts
+    int ng;
+};
+void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s);
 
 // --------------------------------------------------- persistent Euler flow --
 // Euler steps first..S-1 of the BC flow (compute_flow_actions) for every active
@@ -301,5 +310,42 @@ struct InitArgs {                 // uniform(-lim, lim) fill of one tensor of on
     unsigned salt;
 };
 void launch_init(const InitArgs& a, hipStream_t s);
+
+// ------------------------------------------- world-model rollout eval ----
+// evaluator/evaluation.py:75-114 on task/offline_task_simulated.py:85-107 for
+// every active member in ONE launch: per step a = clip(onestep(s, z)),
+// s' = BaselineStatePredictor(s, a) (envmodel/baseline.py:25-37: LayerNorm of
+// [s, a], Dense+ReLU hidden layers, Dense(obs) + s), terminated =
+// TerminationPredictor(s') > 0 (envmodel/termination_predictor.py:14-21),
+// until every env has terminated or max_steps.  Block = 16 envs of one member.
+constexpr int RO_MAX_LAYERS = 8;   // env-model Dense layers (hidden + output)
+constexpr int RO_MAX_W = 512;      // widest env-model layer
+struct RolloutArgs {
+    const float* params;           // population arena (slot stride P), one-step actor at os_off
+    long long P, os_off;
+    long long w_off[EF_MAX_LAYERS + 1], b_off[EF_MAX_LAYERS + 1];
+    int D, A, L;                   // actor hidden width 512
+    const float* sp;               // state predictor params (flat, flax order)
+    int sp_n;                      // Dense layers (hidden + output)
+    int sp_dims[RO_MAX_LAYERS + 1];
+    long long sp_w[RO_MAX_LAYERS], sp_b[RO_MAX_LAYERS], sp_ln_scale, sp_ln_bias;
+    const float* tp;               // termination predictor params
+    int tp_n;
+    int tp_dims[RO_MAX_LAYERS + 1];
+    long long tp_w[RO_MAX_LAYERS], tp_b[RO_MAX_LAYERS];
+    const float* init_obs;         // [n_envs][D]
+    int n_envs, max_steps;
+    uint64_t seed;
+    const uint64_t* member_seeds;  // per slot
+    const float* noise;            // null or [nz][max_steps][n_envs][A]
+    float* out;                    // [nz][n_envs][2]: success, episode length
+    float* out_obs;                // null or [nz][n_envs][D]: observation after the last step
+    const float* actions;          // non-null: env-model step only, a = actions [n_envs][A] (no actor)
+    float* out_logit;              // null or [nz][n_envs]: termination logit of the last step
+    int nz;
+    const int* slots;
+};
+bool rollout_supported(int H, int L, int D, int A);
+void launch_rollout(const RolloutArgs& a, hipStream_t s);
 
 }  // namespace fq

@@ -149,19 +149,22 @@ DEV void stage_store(float* __restrict__ S, int p, float4 v) {
     }
 }
 
+template <int BM, int BN, int BK, bool ARC, bool BRC>
+constexpr int gemm_smem_floats() {
+    return 2 * ((ARC ? BM * (BK + 1) : BK * BM) + (BRC ? BN * (BK + 1) : BK * BN)) + BM;
+}
+
+// One output tile (logical block id w of the problem g) of the register-staged GEMM.
 template <int BM, int BN, int BK, bool DUAL, bool ARC, bool BRC, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
+DEV void gemm_body(const GemmArgs& g, int w, float* smem) {
     constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
     constexpr int A_SZ = ARC ? BM * (BK + 1) : BK * BM;
     constexpr int B_SZ = BRC ? BN * (BK + 1) : BK * BN;
     constexpr int A_LD = BM * BK / 1024;  // float4 loads per thread
     constexpr int B_LD = BN * BK / 1024;
-    __shared__ __attribute__((aligned(16))) float smem[2 * (A_SZ + B_SZ) + BM];
 
     const int tiles_m = g.M / BM + (g.M % BM != 0), tiles_n = g.N / BN;  // host guarantees N % BN == 0
     const int per = tiles_m * tiles_n;
-    const int total = per * g.ny * g.nz;
-    const int w = xcd_remap(blockIdx.x, total);
     const int tile = w % per, yz = w / per;
     const int y = yz % g.ny, z = yz / g.ny;
     const int slot = g.slots[z];
@@ -299,6 +302,46 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
                     }
                 }
             }
+    }
+}
+
+template <int BM, int BN, int BK, bool DUAL, bool ARC, bool BRC, int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
+    __shared__ __attribute__((aligned(16))) float smem[gemm_smem_floats<BM, BN, BK, ARC, BRC>()];
+    const int tiles_m = g.M / BM + (g.M % BM != 0), tiles_n = g.N / BN;
+    const int total = tiles_m * tiles_n * g.ny * g.nz;
+    gemm_body<BM, BN, BK, DUAL, ARC, BRC, EPI>(g, xcd_remap(blockIdx.x, total), smem);
+}
+
+// Grouped launch of independent problems of one layout (the dW GEMMs of every
+// layer of a network): block -> problem by the prefix of tile counts.
+template <int BM, int BN, bool ARC, bool BRC>
+__global__ __launch_bounds__(256, 2) void gemm_group_kernel(const GemmGroupArgs ga) {
+    __shared__ __attribute__((aligned(16))) float smem[gemm_smem_floats<BM, BN, 32, ARC, BRC>()];
+    const int bid = xcd_remap(blockIdx.x, ga.first[ga.ng]);
+    int gi = 0;
+#pragma unroll
+    for (int i = 1; i < GEMM_GROUP_MAX; ++i)
+        if (i < ga.ng && bid >= ga.first[i]) gi = i;
+    gemm_body<BM, BN, 32, false, ARC, BRC, EPI_STORE>(ga.g[gi], bid - ga.first[gi], smem);
+}
+
+void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s) {
+    GemmGroupArgs ga{};
+    const int bm = (tile & 1) ? 128 : 64, bn = (tile & 2) ? 128 : 64;
+    int tot = 0;
+    for (int i = 0; i < ng; ++i) {
+        ga.g[i] = gs[i];
+        ga.first[i] = tot;
+        tot += ((gs[i].M + bm - 1) / bm) * (gs[i].N / bn) * gs[i].ny * gs[i].nz;
+    }
+    ga.first[ng] = tot;
+    ga.ng = ng;
+    switch (tile) {
+        case 0: hipLaunchKernelGGL((gemm_group_kernel<64, 64, true, true>), dim3(tot), dim3(256), 0, s, ga); break;
+        case 1: hipLaunchKernelGGL((gemm_group_kernel<128, 64, true, true>), dim3(tot), dim3(256), 0, s, ga); break;
+        case 2: hipLaunchKernelGGL((gemm_group_kernel<64, 128, true, true>), dim3(tot), dim3(256), 0, s, ga); break;
+        default: hipLaunchKernelGGL((gemm_group_kernel<128, 128, true, true>), dim3(tot), dim3(256), 0, s, ga); break;
     }
 }
 
@@ -2037,6 +2080,277 @@ __global__ __launch_bounds__(256) void init_kernel(const InitArgs a) {
 void launch_init(const InitArgs& a, hipStream_t s) {
     if (a.n <= 0) return;
     hipLaunchKernelGGL(init_kernel, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+}
+
+// ============================================== world-model rollout eval ==
+// (RolloutArgs, kernels.h)  One block = 16 envs (columns) of one member for
+// the whole episode; every network runs on LDS-resident activations:
+//   actor   - the streamed 512-wide k-loop of stream_fwd (weights from L2),
+//             GELU, head -> clip: sample_actions (evaluator/evaluation.py:58-64)
+//   s'      - LayerNorm over [s, a] per column, Dense+ReLU..., Dense(D) + s
+//   term    - Dense+ReLU..., Dense(1) > 0
+// Small Dense layers: 16-feature output tiles round-robin over the 8 waves,
+// v_mfma_f32_16x16x4_f32 with W rows from L2 and x from LDS.
+bool rollout_supported(int H, int L, int D, int A) {
+    return H == EF_H && L >= 1 && L <= EF_MAX_LAYERS && D + A <= EF_K0MAX && A <= 8 && D <= 64;
+}
+
+// y[o][c] = act(sum_k W[k][o] x[k][c] + b[o]), o < Wo, k < Wi, c < 16 (LDS in / out,
+// row pitch 16); res (optional, LDS [Wo][16]) is added after the activation.
+template <bool RELU>
+DEV void ro_dense(const float* __restrict__ W, const float* __restrict__ bias, const float* xin, int Wi, int Wo,
+                  float* yout, const float* res, int w, int li, int lk) {
+    const int ntile = (Wo + 15) / 16, nks = (Wi + 3) / 4;
+    for (int t = w; t < ntile; t += EF_NW) {
+        const int o = 16 * t + li;
+        const int oc = o < Wo ? o : Wo - 1;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        int s = 0;
+        for (; s + 4 <= nks; s += 4) {
+            float av[4], bv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = 4 * (s + u) + lk;
+                const int kc = k < Wi ? k : Wi - 1;
+                av[u] = (k < Wi && o < Wo) ? W[(long long)kc * Wo + oc] : 0.f;
+                bv[u] = k < Wi ? xin[kc * EF_NC + li] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+        }
+        for (; s < nks; ++s) {
+            const int k = 4 * s + lk;
+            const int kc = k < Wi ? k : Wi - 1;
+            const float av = (k < Wi && o < Wo) ? W[(long long)kc * Wo + oc] : 0.f;
+            const float bv = k < Wi ? xin[kc * EF_NC + li] : 0.f;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+        }
+        // acc[r]: feature 16t + 4lk + r, column li
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int f = 16 * t + 4 * lk + r;
+            if (f < Wo) {
+                float v = acc[r] + bias[f];
+                if (RELU) v = fmaxf(v, 0.f);
+                if (res) v += res[f * EF_NC + li];
+                yout[f * EF_NC + li] = v;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(EF_NW * 64, 1) void rollout_kernel(const RolloutArgs g) {
+    constexpr int H = EF_H, NC = EF_NC, NT = EF_NW * 64, PF = EF_PF;
+    __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];
+    __shared__ __attribute__((aligned(16))) float in0[EF_K0MAX * NC + 64];   // actor input [s; z]
+    __shared__ __attribute__((aligned(16))) float bufA[RO_MAX_W * NC];
+    __shared__ __attribute__((aligned(16))) float bufB[RO_MAX_W * NC];
+    __shared__ float obs_s[64 * NC], obs_n[64 * NC], act_s[8 * NC];
+    __shared__ float hred[EF_NW * 8 * NC];
+    __shared__ float lnp[2][NC];
+    __shared__ int done_s[NC];
+    __shared__ float res_s[NC][2];
+    __shared__ int all_done;
+
+    const int ntile = (g.n_envs + NC - 1) / NC;
+    const int bid = blockIdx.x;
+    const int z = bid / ntile, e0 = (bid % ntile) * NC;
+    const int slot = g.slots[z];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    const int D = g.D, A = g.A, L = g.L, K0 = D + A;
+    const int NS0 = (K0 + 4 * PF - 1) / (4 * PF) * PF;
+    const float* __restrict__ P = g.params + (long long)slot * g.P + g.os_off;
+    const uint64_t key = g.seed ^ (g.member_seeds[slot] * 0x9E3779B97F4A7C15ull);
+
+    for (int e = tid; e < EF_K0MAX * NC + 64; e += NT) in0[e] = 0.f;
+    for (int e = tid; e < 64 * NC; e += NT) {
+        const int k = e / NC, c = e % NC;
+        obs_s[e] = (k < D && e0 + c < g.n_envs) ? g.init_obs[(long long)(e0 + c) * D + k] : 0.f;
+    }
+    if (tid < NC) {
+        done_s[tid] = e0 + tid >= g.n_envs;  // padding columns are done from the start
+        res_s[tid][0] = 0.f;
+        res_s[tid][1] = 0.f;
+    }
+    const rsrc_t rW = make_rsrc(P, g.P - g.os_off);
+    const int lo = lk * H + 64 * w + 4 * li;
+    float4 ring[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) ring[p] = bload4(rW, (int)g.w_off[0] + 4 * p * H + lo);
+    float w5r[16];  // head A fragments: W_L[64w + 4s + lk][li], li < A
+#pragma unroll
+    for (int s = 0; s < 16; ++s) w5r[s] = li < A ? P[g.w_off[L] + (64 * w + 4 * s + lk) * A + li] : 0.f;
+    __syncthreads();
+
+    for (int t = 1; t <= g.max_steps; ++t) {
+      if (g.actions) {  // env-model step only (fqlpop_envmodel_step): given actions
+        if (tid < A * NC) {
+            const int j = tid / NC, c = tid % NC;
+            act_s[tid] = e0 + c < g.n_envs ? g.actions[(long long)(e0 + c) * A + j] : 0.f;
+        }
+        __syncthreads();
+      } else {
+        // ---- actor input [s; z_t] ----------------------------------------
+        for (int e = tid; e < K0 * NC; e += NT) {
+            const int k = e / NC;
+            if (k < D) in0[e] = obs_s[e];
+        }
+        if (tid < NC * ((A + 1) / 2)) {
+            const int c = tid % NC, q = tid / NC;  // normal pair q: actions 2q, 2q+1
+            float n0, n1;
+            if (g.noise) {
+                const float* nz = g.noise + (((long long)z * g.max_steps + (t - 1)) * g.n_envs + e0 + c) * A;
+                const bool ok = e0 + c < g.n_envs;
+                n0 = ok ? nz[2 * q] : 0.f;
+                n1 = (ok && 2 * q + 1 < A) ? nz[2 * q + 1] : 0.f;
+            } else {
+                uint32_t cc[4] = {(uint32_t)(e0 + c), (uint32_t)t, 0x5E11u, (uint32_t)q};
+                philox4x32_10(cc, (uint32_t)key, (uint32_t)(key >> 32));
+                const float r = sqrtf(-2.0f * logf(u01_open_closed(cc[0])));
+                float sv, cv;
+                sincosf(6.283185307179586f * u01(cc[1]), &sv, &cv);
+                n0 = r * cv;
+                n1 = r * sv;
+            }
+            in0[(D + 2 * q) * NC + c] = n0;
+            if (2 * q + 1 < A) in0[(D + 2 * q + 1) * NC + c] = n1;
+        }
+        __syncthreads();
+        // ---- actor hidden layers (streamed weights, GELU) -----------------
+        for (int l = 0; l < L; ++l) {
+            const int NS = l == 0 ? NS0 : H / 4;
+            const float* xs = l == 0 ? in0 : slab;
+            const int nl = l + 1 < L ? l + 1 : 0;
+            f32x4 acc[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+            float4 bias4[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bias4[r] = bload4(rW, (int)g.b_off[l] + 64 * w + 16 * lk + 4 * r);
+            ef_kloop(acc, ring, rW, xs, NS, (int)g.w_off[l], (int)g.w_off[nl], lo, lk, li);
+            __syncthreads();  // every wave done reading the slab
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float bb[4] = {bias4[r].x, bias4[r].y, bias4[r].z, bias4[r].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    slab[(64 * w + 16 * lk + 4 * r + c) * NC + li] = gelu_fast(acc[c][r] + bb[c]);
+            }
+            __syncthreads();
+        }
+        // ---- head: a = clip(W_L^T h + b_L) ---------------------------------
+        {
+            f32x4 hacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(w5r[s], slab[(64 * w + 4 * s + lk) * NC + li], hacc, 0, 0, 0);
+            if (lk < 2) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) hred[w * 8 * NC + (4 * lk + r) * NC + li] = hacc[r];
+            }
+            __syncthreads();
+            if (tid < A * NC) {
+                const int j = tid / NC;
+                float v = hred[tid];
+#pragma unroll
+                for (int q = 1; q < EF_NW; ++q) v += hred[q * 8 * NC + tid];
+                act_s[tid] = clip1(v + P[g.b_off[L] + j]);
+            }
+            __syncthreads();
+        }
+      }
+        // ---- state predictor: LayerNorm([s, a]) -> Dense+ReLU ... -> Dense(D) + s
+        if (tid < NC) {
+            float s1 = 0.f, s2 = 0.f;
+            for (int k = 0; k < K0; ++k) {
+                const float x = k < D ? obs_s[k * NC + tid] : act_s[(k - D) * NC + tid];
+                s1 += x;
+                s2 += x * x;
+            }
+            const float mean = s1 / (float)K0;
+            const float var = fmaxf(s2 / (float)K0 - mean * mean, 0.f);
+            lnp[0][tid] = mean;
+            lnp[1][tid] = 1.0f / sqrtf(var + 1e-6f);
+        }
+        __syncthreads();
+        for (int e = tid; e < K0 * NC; e += NT) {
+            const int k = e / NC, c = e % NC;
+            const float x = k < D ? obs_s[e] : act_s[(k - D) * NC + c];
+            bufA[e] = (x - lnp[0][c]) * lnp[1][c] * g.sp[g.sp_ln_scale + k] + g.sp[g.sp_ln_bias + k];
+        }
+        __syncthreads();
+        {
+            float* cur = bufA;
+            float* nxt = bufB;
+            for (int i = 0; i < g.sp_n; ++i) {
+                const bool last = i == g.sp_n - 1;
+                if (last)
+                    ro_dense<false>(g.sp + g.sp_w[i], g.sp + g.sp_b[i], cur, g.sp_dims[i], g.sp_dims[i + 1], obs_n,
+                                    obs_s, w, li, lk);
+                else
+                    ro_dense<true>(g.sp + g.sp_w[i], g.sp + g.sp_b[i], cur, g.sp_dims[i], g.sp_dims[i + 1], nxt,
+                                   nullptr, w, li, lk);
+                __syncthreads();
+                float* tmp = cur; cur = nxt; nxt = tmp;
+            }
+        }
+        // ---- termination predictor on s' ----------------------------------
+        {
+            const float* cur = obs_n;
+            for (int i = 0; i < g.tp_n; ++i) {
+                float* dst = (i & 1) ? bufB : bufA;
+                if (i == g.tp_n - 1)
+                    ro_dense<false>(g.tp + g.tp_w[i], g.tp + g.tp_b[i], cur, g.tp_dims[i], g.tp_dims[i + 1], dst,
+                                    nullptr, w, li, lk);
+                else
+                    ro_dense<true>(g.tp + g.tp_w[i], g.tp + g.tp_b[i], cur, g.tp_dims[i], g.tp_dims[i + 1], dst,
+                                   nullptr, w, li, lk);
+                __syncthreads();
+                cur = dst;
+            }
+            if (g.out_logit && tid < NC && e0 + tid < g.n_envs) g.out_logit[(long long)z * g.n_envs + e0 + tid] = cur[tid];
+            // ---- bookkeeping (evaluate_actor_fn: first terminated / truncated step)
+            if (tid < NC) {
+                if (!done_s[tid]) {
+                    if (cur[tid] > 0.f) {
+                        res_s[tid][0] = 1.f;
+                        res_s[tid][1] = (float)t;
+                        done_s[tid] = 1;
+                    } else if (t >= g.max_steps) {
+                        res_s[tid][1] = (float)t;
+                        done_s[tid] = 1;
+                    }
+                }
+            }
+        }
+        for (int e = tid; e < 64 * NC; e += NT) obs_s[e] = obs_n[e];
+        __syncthreads();
+        if (tid == 0) {
+            int a = 1;
+            for (int c = 0; c < NC; ++c) a &= done_s[c];
+            all_done = a;
+        }
+        __syncthreads();
+        if (all_done) break;
+    }
+    if (tid < NC && e0 + tid < g.n_envs) {
+        float* o = g.out + ((long long)z * g.n_envs + e0 + tid) * 2;
+        o[0] = res_s[tid][0];
+        o[1] = res_s[tid][1];
+    }
+    if (g.out_obs) {
+        for (int e = tid; e < D * NC; e += NT) {
+            const int k = e / NC, c = e % NC;
+            if (e0 + c < g.n_envs) g.out_obs[((long long)z * g.n_envs + e0 + c) * D + k] = obs_s[e];
+        }
+    }
+}
+
+void launch_rollout(const RolloutArgs& a, hipStream_t s) {
+    const dim3 grid(((a.n_envs + EF_NC - 1) / EF_NC) * a.nz);
+    hipLaunchKernelGGL(rollout_kernel, grid, dim3(EF_NW * 64), 0, s, a);
 }
 
 }  // namespace fq

@@ -175,6 +175,11 @@ struct fqlpop {
     float* paramsT = nullptr;
     long long PTT = 0, wt_net_off[3] = {0, 0, 0};
     bool wt_dirty = true;          // params changed on the host side: re-transpose before the next step
+    // world-model rollout evaluator (fqlpop_set_env_model / fqlpop_rollout)
+    fqlpop_envmodel_config em{};
+    float *sp_params = nullptr, *tp_params = nullptr;
+    RolloutArgs em_args{};
+    bool em_set = false;
     bool probe = false;
     int probe_set = -1;            // set used by the step being enqueued (-1: none)
     int probe_idx = 0;             // next launch slot of that set
@@ -569,7 +574,9 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
     r.L = N.L; r.H = N.H; r.ln = N.ln ? 1 : 0;
     r.ny = N.E; r.nz = c.nz; r.slots = h->slots;
     launch_colsum_reduce(r, sw);
+    // dW_l = X_l^T du_l over the first Mg columns, every layer in one grouped launch
     auto act = [&](float* p) { return tref(p + coff, act_ss, act_sy); };
+    std::vector<GemmArgs> gs;
     for (int l = N.L - 1; l >= 0; --l) {
         GemmArgs gw{};
         gw.A = l == 0 ? X0 : act(G[l - 1]);
@@ -578,7 +585,12 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         gw.M = N.kdim(l); gw.N = N.H; gw.K = Mg;
         gw.lda = ld; gw.ldb = ld_d; gw.ldc = N.H;
         gw.ny = N.E; gw.nz = c.nz; gw.slots = h->slots;
-        gemm(LAYOUT_DW, EPI_STORE, gw, sw);
+        gs.push_back(gw);
+    }
+    if (N.L <= GEMM_GROUP_MAX && N.H % 128 == 0) {
+        launch_gemm_group_dw(N.E > 1 ? 3 : 2, gs.data(), (int)gs.size(), sw);
+    } else {
+        for (const GemmArgs& gw : gs) gemm(LAYOUT_DW, EPI_STORE, gw, sw);
     }
 }
 
@@ -1249,7 +1261,8 @@ int fqlpop_destroy(fqlpop_t* h) {
         for (float* p : h->allocs) (void)hipFree(p);
         for (void* p : {(void*)h->params, (void*)h->grads, (void*)h->adam_m, (void*)h->adam_v, (void*)h->target,
                         (void*)h->count, (void*)h->seeds, (void*)h->alpha, (void*)h->slots, (void*)h->stats,
-                        (void*)h->chunks, (void*)h->chunk_leaf, (void*)h->leaf_first})
+                        (void*)h->chunks, (void*)h->chunk_leaf, (void*)h->leaf_first, (void*)h->sp_params,
+                        (void*)h->tp_params})
             if (p) (void)hipFree(p);
         for (auto& d : h->ds)
             for (float* p : {d.obs, d.act, d.rew, d.mask, d.nobs})
@@ -1662,3 +1675,151 @@ int fqlpop_read_probe(fqlpop_t* h, double* total_us, int64_t* launches, double* 
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ env model
+namespace {
+// Offsets of the flax-ordered env-model leaves; returns the float count.
+// dims: in, hidden..., out.  ln: BaselineStatePredictor (LayerNorm_0 after the Dense leaves).
+long long envmodel_layout(const std::vector<int>& dims, bool ln, long long* w, long long* b, long long* ln_bias,
+                          long long* ln_scale) {
+    long long o = 0;
+    for (size_t i = 0; i + 1 < dims.size(); ++i) {
+        b[i] = o; o += dims[i + 1];                          // Dense_i/bias
+        w[i] = o; o += (long long)dims[i] * dims[i + 1];     // Dense_i/kernel
+    }
+    if (ln) {
+        *ln_bias = o; o += dims[0];                          // LayerNorm_0/bias
+        *ln_scale = o; o += dims[0];                         // LayerNorm_0/scale
+    }
+    return o;
+}
+
+void envmodel_dims(const fqlpop_envmodel_config* c, std::vector<int>& sp, std::vector<int>& tp) {
+    ARGCHK(c->obs_dim > 0 && c->action_dim > 0, "bad env-model dims");
+    ARGCHK(c->sp_num_hidden >= 0 && c->sp_num_hidden < RO_MAX_LAYERS && c->tp_num_hidden >= 0 &&
+               c->tp_num_hidden < RO_MAX_LAYERS, "too many env-model layers");
+    sp = {c->obs_dim + c->action_dim};
+    for (int i = 0; i < c->sp_num_hidden; ++i) sp.push_back(c->sp_hidden[i]);
+    sp.push_back(c->obs_dim);
+    tp = {c->obs_dim};
+    for (int i = 0; i < c->tp_num_hidden; ++i) tp.push_back(c->tp_hidden[i]);
+    tp.push_back(1);
+    for (int d : sp) ARGCHK(d > 0 && d <= RO_MAX_W, "env-model layer width must be in 1..512");
+    for (int d : tp) ARGCHK(d > 0 && d <= RO_MAX_W, "env-model layer width must be in 1..512");
+}
+}  // namespace
+
+int fqlpop_envmodel_param_count(const fqlpop_envmodel_config* cfg, int64_t* n_sp, int64_t* n_tp) {
+    return guard([&] {
+        ARGCHK(cfg && n_sp && n_tp, "null argument");
+        std::vector<int> sp, tp;
+        envmodel_dims(cfg, sp, tp);
+        long long w[RO_MAX_LAYERS], b[RO_MAX_LAYERS], lb = 0, ls = 0;
+        *n_sp = envmodel_layout(sp, true, w, b, &lb, &ls);
+        *n_tp = envmodel_layout(tp, false, w, b, &lb, &ls);
+    });
+}
+
+int fqlpop_set_env_model(fqlpop_t* h, const fqlpop_envmodel_config* cfg, const float* sp_params, int64_t n_sp,
+                         const float* tp_params, int64_t n_tp) {
+    return guard([&] {
+        ARGCHK(h && cfg && sp_params && tp_params, "null argument");
+        ARGCHK(cfg->obs_dim == h->D && cfg->action_dim == h->A, "env-model obs/action dims differ from the agent's");
+        std::vector<int> sp, tp;
+        envmodel_dims(cfg, sp, tp);
+        RolloutArgs& r = h->em_args;
+        r = RolloutArgs{};
+        const long long nsp = envmodel_layout(sp, true, r.sp_w, r.sp_b, &r.sp_ln_bias, &r.sp_ln_scale);
+        long long lb = 0, ls = 0;
+        const long long ntp = envmodel_layout(tp, false, r.tp_w, r.tp_b, &lb, &ls);
+        ARGCHK(n_sp == nsp && n_tp == ntp, "env-model parameter count mismatch (fqlpop_envmodel_param_count)");
+        r.sp_n = (int)sp.size() - 1;
+        r.tp_n = (int)tp.size() - 1;
+        for (size_t i = 0; i < sp.size(); ++i) r.sp_dims[i] = sp[i];
+        for (size_t i = 0; i < tp.size(); ++i) r.tp_dims[i] = tp[i];
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipDeviceSynchronize());
+        if (h->sp_params) (void)hipFree(h->sp_params);
+        if (h->tp_params) (void)hipFree(h->tp_params);
+        h->sp_params = h->tp_params = nullptr;
+        HIPCHK(hipMalloc(&h->sp_params, sizeof(float) * nsp));
+        HIPCHK(hipMalloc(&h->tp_params, sizeof(float) * ntp));
+        HIPCHK(hipMemcpy(h->sp_params, sp_params, sizeof(float) * nsp, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(h->tp_params, tp_params, sizeof(float) * ntp, hipMemcpyHostToDevice));
+        h->em = *cfg;
+        h->em_set = true;
+    });
+}
+
+int fqlpop_rollout(fqlpop_t* h, const float* init_obs, int n_envs, int max_steps, uint64_t seed, const float* noise,
+                   float* out, float* out_obs) {
+    return guard([&] {
+        ARGCHK(h && init_obs && out, "null argument");
+        ARGCHK(n_envs > 0 && max_steps > 0, "n_envs and max_steps must be positive");
+        if (!h->em_set) throw FqErr{FQLPOP_E_STATE, "no env model set (fqlpop_set_env_model)"};
+        if (!rollout_supported(h->H, h->L, h->D, h->A))
+            throw FqErr{FQLPOP_E_UNSUPPORTED, "rollout needs hidden_dim 512, obs_dim + action_dim <= 64"};
+        if (h->os.ln) throw FqErr{FQLPOP_E_UNSUPPORTED, "rollout with actor_layer_norm is not supported"};
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipStreamSynchronize(h->sM));
+        const int nz = h->nz, D = h->D, A = h->A;
+        if (nz == 0) return;
+        RolloutArgs r = h->em_args;
+        r.params = h->params; r.P = h->P; r.os_off = h->os.off;
+        for (int l = 0; l <= h->L; ++l) { r.w_off[l] = h->os.W[l]; r.b_off[l] = h->os.b[l]; }
+        r.D = D; r.A = A; r.L = h->L;
+        r.sp = h->sp_params; r.tp = h->tp_params;
+        r.n_envs = n_envs; r.max_steps = max_steps; r.seed = seed; r.member_seeds = h->seeds;
+        r.nz = nz; r.slots = h->slots;
+        float *d_obs = nullptr, *d_noise = nullptr, *d_out = nullptr, *d_oobs = nullptr;
+        const size_t n_noise = (size_t)nz * max_steps * n_envs * A;
+        HIPCHK(hipMalloc(&d_obs, sizeof(float) * n_envs * D));
+        HIPCHK(hipMalloc(&d_out, sizeof(float) * nz * n_envs * 2));
+        HIPCHK(hipMemcpy(d_obs, init_obs, sizeof(float) * n_envs * D, hipMemcpyHostToDevice));
+        if (noise) {
+            HIPCHK(hipMalloc(&d_noise, sizeof(float) * n_noise));
+            HIPCHK(hipMemcpy(d_noise, noise, sizeof(float) * n_noise, hipMemcpyHostToDevice));
+        }
+        if (out_obs) HIPCHK(hipMalloc(&d_oobs, sizeof(float) * nz * n_envs * D));
+        r.init_obs = d_obs; r.noise = d_noise; r.out = d_out; r.out_obs = d_oobs;
+        launch_rollout(r, h->sM);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(h->sM));
+        HIPCHK(hipMemcpy(out, d_out, sizeof(float) * nz * n_envs * 2, hipMemcpyDeviceToHost));
+        if (out_obs) HIPCHK(hipMemcpy(out_obs, d_oobs, sizeof(float) * nz * n_envs * D, hipMemcpyDeviceToHost));
+        for (float* p : {d_obs, d_noise, d_out, d_oobs})
+            if (p) (void)hipFree(p);
+    });
+}
+
+int fqlpop_envmodel_step(fqlpop_t* h, const float* obs, const float* actions, int n, float* next_obs, float* logits) {
+    return guard([&] {
+        ARGCHK(h && obs && actions && next_obs && logits && n > 0, "bad argument");
+        if (!h->em_set) throw FqErr{FQLPOP_E_STATE, "no env model set (fqlpop_set_env_model)"};
+        ARGCHK(h->D + h->A <= 64 && h->D <= 64 && h->A <= 8, "obs_dim + action_dim must be <= 64");
+        HIPCHK(hipSetDevice(h->device));
+        HIPCHK(hipStreamSynchronize(h->sM));
+        const int D = h->D, A = h->A;
+        RolloutArgs r = h->em_args;
+        r.params = h->params; r.P = h->P; r.os_off = h->os.off;
+        r.D = D; r.A = A; r.L = h->L;
+        r.sp = h->sp_params; r.tp = h->tp_params;
+        r.n_envs = n; r.max_steps = 1; r.seed = 0; r.member_seeds = h->seeds;
+        r.nz = 1; r.slots = h->slots;  // any slot: the actor is not run
+        float *d_obs = nullptr, *d_act = nullptr, *d_out = nullptr, *d_oobs = nullptr, *d_logit = nullptr;
+        HIPCHK(hipMalloc(&d_obs, sizeof(float) * n * D));
+        HIPCHK(hipMalloc(&d_act, sizeof(float) * n * A));
+        HIPCHK(hipMalloc(&d_out, sizeof(float) * n * 2));
+        HIPCHK(hipMalloc(&d_oobs, sizeof(float) * n * D));
+        HIPCHK(hipMalloc(&d_logit, sizeof(float) * n));
+        HIPCHK(hipMemcpy(d_obs, obs, sizeof(float) * n * D, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d_act, actions, sizeof(float) * n * A, hipMemcpyHostToDevice));
+        r.init_obs = d_obs; r.actions = d_act; r.out = d_out; r.out_obs = d_oobs; r.out_logit = d_logit;
+        launch_rollout(r, h->sM);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(h->sM));
+        HIPCHK(hipMemcpy(next_obs, d_oobs, sizeof(float) * n * D, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(logits, d_logit, sizeof(float) * n, hipMemcpyDeviceToHost));
+        for (float* p : {d_obs, d_act, d_out, d_oobs, d_logit}) (void)hipFree(p);
+    });
+}

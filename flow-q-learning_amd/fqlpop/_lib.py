@@ -48,6 +48,15 @@ class Config(ctypes.Structure):
     ]
 
 
+class EnvModelConfig(ctypes.Structure):
+    """Mirror of ``fqlpop_envmodel_config`` (include/fqlpop.h)."""
+    _fields_ = [
+        ("obs_dim", ctypes.c_int), ("action_dim", ctypes.c_int),
+        ("sp_num_hidden", ctypes.c_int), ("sp_hidden", ctypes.c_int * 7),
+        ("tp_num_hidden", ctypes.c_int), ("tp_hidden", ctypes.c_int * 7),
+    ]
+
+
 _P = ctypes.c_void_p
 _F = ctypes.POINTER(ctypes.c_float)
 _SIGS = {
@@ -88,6 +97,12 @@ _SIGS = {
                                                    ctypes.POINTER(ctypes.c_double)]),
     "fqlpop_read_probe": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                          ctypes.POINTER(ctypes.c_double)]),
+    "fqlpop_envmodel_param_count": (ctypes.c_int, [ctypes.POINTER(EnvModelConfig), ctypes.POINTER(ctypes.c_int64),
+                                                   ctypes.POINTER(ctypes.c_int64)]),
+    "fqlpop_set_env_model": (ctypes.c_int, [_P, ctypes.POINTER(EnvModelConfig), _F, ctypes.c_int64, _F,
+                                            ctypes.c_int64]),
+    "fqlpop_rollout": (ctypes.c_int, [_P, _F, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, _F, _F, _F]),
+    "fqlpop_envmodel_step": (ctypes.c_int, [_P, _F, _F, ctypes.c_int, _F, _F]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
 

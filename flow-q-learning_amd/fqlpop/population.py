@@ -244,6 +244,61 @@ class Population:
                                              ctypes.c_uint64(int(seed) & (2**64 - 1)), fptr(out)))
         return out[0] if squeeze else out
 
+    # ------------------------------------------------------ world-model eval
+    def set_env_model(self, sp_flat, tp_flat, sp_hidden=(128, 256, 128), tp_hidden=(128, 128)):
+        """Upload a BaselineStatePredictor / TerminationPredictor pair as flat
+        flax-ordered parameter vectors (envmodel.flatten_state_predictor / ...)."""
+        c = _lib.EnvModelConfig()
+        c.obs_dim, c.action_dim = self.cfg.obs_dim, self.cfg.action_dim
+        c.sp_num_hidden = len(sp_hidden)
+        c.tp_num_hidden = len(tp_hidden)
+        for i, d in enumerate(sp_hidden):
+            c.sp_hidden[i] = int(d)
+        for i, d in enumerate(tp_hidden):
+            c.tp_hidden[i] = int(d)
+        n_sp, n_tp = ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.fqlpop_envmodel_param_count(ctypes.byref(c), ctypes.byref(n_sp), ctypes.byref(n_tp)))
+        sp = _f32(sp_flat).reshape(-1)
+        tp = _f32(tp_flat).reshape(-1)
+        if sp.shape[0] != n_sp.value or tp.shape[0] != n_tp.value:
+            raise ValueError(f"env-model sizes {sp.shape[0]}/{tp.shape[0]} != expected {n_sp.value}/{n_tp.value}")
+        check(self.lib.fqlpop_set_env_model(self._h, ctypes.byref(c), fptr(sp), sp.shape[0], fptr(tp), tp.shape[0]))
+        self._em_cfg = c
+
+    def rollout(self, init_obs, max_steps: int, seed: int = 0, noise=None, return_obs: bool = False):
+        """World-model evaluation of every ACTIVE member in one launch.
+
+        Returns (success [n_active, n_envs], lengths [n_active, n_envs]) and,
+        with return_obs, the observations after the last step [n_active, n_envs, obs]."""
+        obs = _f32(init_obs).reshape(-1, self.cfg.obs_dim)
+        n_envs = obs.shape[0]
+        na = len(self.active_ids)
+        nz = None
+        if noise is not None:
+            nz = _f32(noise).reshape(na, int(max_steps), n_envs, self.cfg.action_dim)
+        out = np.zeros((na, n_envs, 2), dtype=np.float32)
+        oobs = np.zeros((na, n_envs, self.cfg.obs_dim), dtype=np.float32) if return_obs else None
+        check(self.lib.fqlpop_rollout(self._h, fptr(obs), n_envs, int(max_steps),
+                                      ctypes.c_uint64(int(seed) & (2**64 - 1)),
+                                      None if nz is None else fptr(nz), fptr(out),
+                                      None if oobs is None else fptr(oobs)))
+        if return_obs:
+            return out[..., 0], out[..., 1], oobs
+        return out[..., 0], out[..., 1]
+
+    def envmodel_step(self, observations, actions):
+        """One state-predictor + termination-predictor step on the GPU:
+        returns (next_observations [n, obs], termination logits [n])."""
+        obs = _f32(observations).reshape(-1, self.cfg.obs_dim)
+        act = _f32(actions).reshape(-1, self.cfg.action_dim)
+        n = obs.shape[0]
+        if act.shape[0] != n:
+            raise ValueError("observations and actions differ in rows")
+        nxt = np.zeros_like(obs)
+        logit = np.zeros(n, dtype=np.float32)
+        check(self.lib.fqlpop_envmodel_step(self._h, fptr(obs), fptr(act), n, fptr(nxt), fptr(logit)))
+        return nxt, logit
+
     # ----------------------------------------------------------------- state
     def get_flat(self, member: int, which: int = STATE_PARAMS) -> np.ndarray:
         flat = np.zeros(self.state_size, dtype=np.float32)

@@ -113,18 +113,29 @@ class Trainer:
                 for e in exps:
                     e.train(self.config.eval_interval)
 
+    def _evaluate_round(self, configs) -> dict:
+        """World-model tasks: every candidate of the round in one GPU rollout
+        (slot -> eval info); other tasks evaluate per experiment."""
+        if not hasattr(self.task, "evaluate_members"):
+            return {}
+        members = [self.member_of[cfg] for cfg in configs if cfg in self.member_of]
+        if not members:
+            return {}
+        return self.task.evaluate_members(self.population, members, int(np.random.randint(0, 2**31 - 1)))
+
     def train(self, max_evaluations: int) -> None:
         while max_evaluations > 0:
             queue = list(self.untrained_candidates) if self.untrained_candidates else list(self.candidates)
             this_round, deferred = queue[:max_evaluations], queue[max_evaluations:]
             start = time.perf_counter()
             self._train_round(this_round)
+            round_eval = self._evaluate_round(this_round)
             for cfg in this_round:
                 exp = self.experiments[cfg]
                 if exp.current_step == exp.steps and cfg not in self.finished_candidates:
                     exp.save_agent()
                     self.finished_candidates.append(cfg)
-                score = exp.evaluate()
+                score = exp.evaluate(round_eval.get(self.member_of.get(cfg)))
                 self.strategy.update(cfg, score)
                 max_evaluations -= 1
             print(f"Elapsed time: {time.perf_counter() - start:.6f} seconds ({len(this_round)} candidates)")

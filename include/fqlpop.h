@@ -180,6 +180,47 @@ int fqlpop_set_probe(fqlpop_t* h, int enable);
 int fqlpop_dominant_kernel_info(fqlpop_t* h, char* name, int name_cap, double* flops, double* bytes);
 int fqlpop_read_probe(fqlpop_t* h, double* total_us, int64_t* launches, double* clock_check);
 
+/* ---------------------------------------------------------------------
+ * World-model rollout evaluation (BASELINE config 5).
+ * Replaces the per-step Python loop of evaluator/evaluation.py:75-114 driving
+ * task/offline_task_simulated.py:85-107 (state predictor + termination
+ * predictor loaded by utils/envmodel.py:10-56) with ONE device launch for all
+ * active members.  Env-model shapes (envmodel/baseline.py:17-37,
+ * envmodel/multistep.py:35-54 uses the same cell, envmodel/termination_predictor.py:9-21). */
+typedef struct fqlpop_envmodel_config {
+    int obs_dim, action_dim;
+    int sp_num_hidden;      /* BaselineStatePredictor hidden_dims (multistep default 128,256,128) */
+    int sp_hidden[7];
+    int tp_num_hidden;      /* TerminationPredictor hidden_dims (default 128,128) */
+    int tp_hidden[7];
+} fqlpop_envmodel_config;
+
+/* Float counts of the flat parameter vectors in flax leaf order:
+ * state predictor  Dense_0/bias, Dense_0/kernel, ..., Dense_n/kernel, LayerNorm_0/bias, LayerNorm_0/scale;
+ * termination      Dense_0/bias, Dense_0/kernel, ..., Dense_m/kernel  (kernels [in][out]). */
+int fqlpop_envmodel_param_count(const fqlpop_envmodel_config* cfg, int64_t* n_sp, int64_t* n_tp);
+
+/* Upload the env model (utils/envmodel.py:load_model for "baseline"/"multistep"
+ * and "termination_predictor"); host arrays, copied. */
+int fqlpop_set_env_model(fqlpop_t* h, const fqlpop_envmodel_config* cfg, const float* sp_params, int64_t n_sp,
+                         const float* tp_params, int64_t n_tp);
+
+/* Roll every ACTIVE member's one-step policy in the env model from init_obs
+ * [n_envs][obs_dim] until each env terminated (termination logit > 0: success 1)
+ * or max_steps (truncated: success 0).  noise: NULL (z ~ N(0,1) from Philox keyed
+ * by seed and the member seed) or host [n_active][max_steps][n_envs][action_dim].
+ * out: host [n_active][n_envs][2] = (success, episode length); out_obs: NULL or
+ * host [n_active][n_envs][obs_dim], the observation after the last step run.
+ * Active members in slot order.  Needs hidden_dim 512; synchronises. */
+int fqlpop_rollout(fqlpop_t* h, const float* init_obs, int n_envs, int max_steps, uint64_t seed,
+                   const float* noise, float* out, float* out_obs);
+
+/* One env-model step for given actions (task/offline_task_simulated.py:85-90:
+ * state_predictor(obs, actions) then termination_predictor(next_obs)): obs
+ * [n][obs_dim], actions [n][action_dim] -> next_obs [n][obs_dim], logits [n]
+ * (terminated = logit > 0).  Host arrays; synchronises. */
+int fqlpop_envmodel_step(fqlpop_t* h, const float* obs, const float* actions, int n, float* next_obs, float* logits);
+
 /* Algorithmic GEMM FLOPs of one member-update at the handle's config
  * (SURVEY.md 8d formula). */
 double fqlpop_flops_per_member_step(const fqlpop_config* cfg);
