@@ -991,8 +991,12 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
         }
         __syncthreads();  // every wave is done reading the slab; lnp visible
 
-        float* __restrict__ U = st && g.U[l] ? g.U[l] + (long long)slot * g.s_ss + (long long)y * g.s_sy : nullptr;
-        float* __restrict__ G = st && g.G[l] ? g.G[l] + (long long)slot * g.s_ss + (long long)y * g.s_sy : nullptr;
+        // activation stores: buffer ops, per-lane offset + wave-uniform row offset (no 64-bit address VGPRs)
+        const bool stU = st && g.U[l], stG = st && g.G[l];
+        const long long sbase = (long long)slot * g.s_ss + (long long)y * g.s_sy + c0;
+        const rsrc_t rU = make_rsrc(stU ? g.U[l] + sbase : g.params, stU ? (long long)H * g.ld_s : 0);
+        const rsrc_t rG = make_rsrc(stG ? g.G[l] + sbase : g.params, stG ? (long long)H * g.ld_s : 0);
+        const int svo = ((64 * w + 16 * lk) * g.ld_s + li) * 4;
         float v[4][4];  // [r][c]: feature 64w + 16lk + 4r + c, column li
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1001,7 +1005,7 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const float u = acc[c][r] + bv[c];
-                if (U) U[(long long)(64 * w + 16 * lk + 4 * r + c) * g.ld_s + m] = u;
+                if (stU) bstore1(rU, u, svo, (4 * r + c) * g.ld_s * 4);
                 v[r][c] = gelu_fast(u);
             }
         }
@@ -1052,7 +1056,7 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const int f = 64 * w + 16 * lk + 4 * r + c;
-                if (G) G[(long long)f * g.ld_s + m] = v[r][c];
+                if (stG) bstore1(rG, v[r][c], svo, (4 * r + c) * g.ld_s * 4);
                 slab[f * NC + li] = v[r][c];
             }
         __syncthreads();
@@ -1371,9 +1375,10 @@ template <bool LN>
 __global__ __launch_bounds__(EF_NW * 64, 1) void stream_bwd_kernel(const StreamBwdArgs g) {
     constexpr int H = EF_H, NC = EF_NC, NT = EF_NW * 64, PF = SB_PF;
     __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];  // du_l [H][NC] (+ look-ahead slack)
-    __shared__ float w5s[H * 8];                                      // head kernel W_L [H][nout]
+    __shared__ __attribute__((aligned(16))) float scr[H * NC];         // head kernel W_L [H][nout]; then LN-grad products
     __shared__ float colred[2][EF_NW][NC];                            // LN column-stat partials per wave
     __shared__ float dos[8][NC];                                      // dout of the block's columns
+    __shared__ __attribute__((aligned(16))) float gams[H];            // LN scale of the current layer
 
     const int tiles = g.M / NC;
     const int total = tiles * g.ny * g.nz;
@@ -1400,7 +1405,7 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_bwd_kernel(const StreamB
         const int j = tid / NC, col = tid % NC;
         dos[j][col] = g.dout[(long long)slot * g.dout_ss + (long long)y * g.dout_sy + (long long)j * g.ld_o + c0 + col];
     }
-    for (int e = tid; e < H * nout; e += NT) w5s[e] = P[g.w_off[L] + e];
+    for (int e = tid; e < H * nout; e += NT) scr[e] = P[g.w_off[L] + e];
     // W^T ring: the first PF k-steps of the first dX product (W_{L-1}^T)
     const int lo = lk * H + 64 * w + 4 * li;
     float4 ring[PF];
@@ -1439,13 +1444,14 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_bwd_kernel(const StreamB
             float s = 0.f;
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                if (j < nout) s += w5s[f * nout + j] * dos[j][li];
+                if (j < nout) s += scr[f * nout + j] * dos[j][li];
             dh[r][c] = s;
         }
+    __syncthreads();  // scr (head kernel image) is reused by the first epilogue
 
     // epilogue inputs of layer l (u, LN stats, LN scale), loaded one layer ahead
     // so that their latency hides under the previous dX product
-    float u[4][4], gam[4][4], mu = 0.f, rs = 0.f;
+    float u[4][4], gth = 0.f, mu = 0.f, rs = 0.f;  // gth: LN scale of feature tid (staged through LDS)
     auto load_epi = [&](int l) {
         const rsrc_t rU = make_rsrc(g.U[l] + so, (long long)H * g.ld_s);
         const int vo = ((64 * w + 16 * lk) * g.ld_s + li) * 4;
@@ -1456,20 +1462,33 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_bwd_kernel(const StreamB
         if constexpr (LN) {
             mu = g.MU[l][sto + li];
             rs = g.RS[l][sto + li];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float4 g4 = *reinterpret_cast<const float4*>(P + g.g_off[l] + 64 * w + 16 * lk + 4 * r);
-                gam[r][0] = g4.x; gam[r][1] = g4.y; gam[r][2] = g4.z; gam[r][3] = g4.w;
-            }
+            gth = P[g.g_off[l] + tid];
         }
     };
     load_epi(L - 1);
+    // parameter-grad partials, thread = feature: sums over the block's 16 columns of an LDS image
+    auto row_sum = [&](const float* a) {
+        const float4* row = reinterpret_cast<const float4*>(&a[tid * NC]);
+        float sv = 0.f;
+#pragma unroll
+        for (int q = 0; q < NC / 4; ++q) {
+            const float4 t4 = row[q];
+            sv += t4.x + t4.y + t4.z + t4.w;
+        }
+        return sv;
+    };
+    // this lane's element (feature 64w + 16lk, column li) of an [H][NC] LDS image; element
+    // (r, c) is at + (4r + c) * NC (ds_write immediate offsets, one address VGPR)
+    const int lofs = (64 * w + 16 * lk) * NC + li;
+    float* const slab_l = slab + lofs;
+    float* const scr_l = scr + lofs;
     for (int l = L - 1; l >= 0; --l) {
-        // ---- du_l from dh = dL/dG_l: GELU' (and LayerNorm backward) --------
-        float du[4][4];
+        // ---- du_l from dh = dL/dG_l (GELU', LayerNorm backward), in place in dh ----
         if constexpr (LN) {
-            // pass 1: xhat, GELU' (kept in u), column partials of dh*gamma and dh*gamma*xhat
-            float xh[4][4], s1 = 0.f, s2 = 0.f;
+            gams[tid] = gth;
+            // pass 1: xhat, GELU' (kept in u); dh and dh * xhat to LDS (LN bias / scale grads;
+            // the slab is free: the previous product is done with it)
+            float xh[4][4];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -1478,18 +1497,34 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_bwd_kernel(const StreamB
                     gelu_and_grad_fast(u[r][c], gv, gpr);
                     u[r][c] = gpr;
                     xh[r][c] = (gv - mu) * rs;
-                    const float dx = dh[r][c] * gam[r][c];
-                    s1 += dx;
-                    s2 += dx * xh[r][c];
+                    scr_l[(4 * r + c) * NC] = dh[r][c];
+                    slab_l[(4 * r + c) * NC] = dh[r][c] * xh[r][c];
                 }
-            // c1[m] = mean_k(dh gamma), c2[m] = mean_k(dh gamma xhat): lk shuffles, waves via LDS
+            __syncthreads();  // gams, scr, slab visible
+            // column partials of dh*gamma and dh*gamma*xhat
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float4 g4 = *reinterpret_cast<const float4*>(&gams[64 * w + 16 * lk + 4 * r]);
+                const float gr[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    dh[r][c] *= gr[c];  // dh * gamma from here on
+                    s1 += dh[r][c];
+                    s2 += dh[r][c] * xh[r][c];
+                }
+            }
             s1 = lk_sum(s1);
             s2 = lk_sum(s2);
             if (lk == 0) {
                 colred[0][w][li] = s1;
                 colred[1][w][li] = s2;
             }
-            __syncthreads();
+            if (gp) {
+                part[(2 * L + l) * H + tid] = row_sum(scr);  // LN bias: sum dh
+                part[(L + l) * H + tid] = row_sum(slab);     // LN scale: sum dh * xhat
+            }
+            __syncthreads();  // colred visible; scr, slab free
             float c1 = 0.f, c2 = 0.f;
 #pragma unroll
             for (int q8 = 0; q8 < EF_NW; ++q8) {
@@ -1498,32 +1533,16 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_bwd_kernel(const StreamB
             }
             c1 = c1 / (float)H;
             c2 = c2 / (float)H;
-            // pass 2: du = rstd (dh gamma - c1 - xhat c2) gelu'(u); LN grads summed over the 16 columns
-            if (gp) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float sgv[4], sbv[4];
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        sgv[c] = row16_sum(dh[r][c] * xh[r][c]);
-                        sbv[c] = row16_sum(dh[r][c]);
-                    }
-                    if (li == 0) {
-                        const int f = 64 * w + 16 * lk + 4 * r;
-                        *reinterpret_cast<float4*>(&part[(L + l) * H + f]) = float4{sgv[0], sgv[1], sgv[2], sgv[3]};
-                        *reinterpret_cast<float4*>(&part[(2 * L + l) * H + f]) = float4{sbv[0], sbv[1], sbv[2], sbv[3]};
-                    }
-                }
-            }
+            // pass 2: du = rstd (dh gamma - c1 - xhat c2) gelu'(u)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) du[r][c] = rs * (dh[r][c] * gam[r][c] - c1 - xh[r][c] * c2) * u[r][c];
+                for (int c = 0; c < 4; ++c) dh[r][c] = rs * (dh[r][c] - c1 - xh[r][c] * c2) * u[r][c];
         } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) du[r][c] = dh[r][c] * gelu_grad_fast(u[r][c]);
+                for (int c = 0; c < 4; ++c) dh[r][c] *= gelu_grad_fast(u[r][c]);
         }
         {
             const rsrc_t rD = make_rsrc(g.DU[l] + dso, (long long)H * g.ld_d);
@@ -1532,21 +1551,12 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_bwd_kernel(const StreamB
             for (int r = 0; r < 4; ++r)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    bstore1(rD, du[r][c], vo, (4 * r + c) * g.ld_d * 4);
-                    slab[(64 * w + 16 * lk + 4 * r + c) * NC + li] = du[r][c];
+                    bstore1(rD, dh[r][c], vo, (4 * r + c) * g.ld_d * 4);
+                    slab_l[(4 * r + c) * NC] = dh[r][c];
                 }
         }
         __syncthreads();
-        if (gp) {  // bias grad partial (thread = feature): sum of du over the block's columns
-            const float4* row = reinterpret_cast<const float4*>(&slab[tid * NC]);
-            float sb = 0.f;
-#pragma unroll
-            for (int q = 0; q < NC / 4; ++q) {
-                const float4 t4 = row[q];
-                sb += t4.x + t4.y + t4.z + t4.w;
-            }
-            part[l * H + tid] = sb;
-        }
+        if (gp) part[l * H + tid] = row_sum(slab);  // bias: sum du
         if (l == 0) break;
 
         // ---- dh_{l-1} = W_l du_l = (W_l^T)^T du_l: the forward k-loop on W_l^T ----
