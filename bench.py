@@ -223,7 +223,7 @@ def main():
     if os.path.exists(args.pmc_json):
         with open(args.pmc_json) as f:
             pmc = json.load(f)
-        if pmc.get("kernel_regex") == kname and pmc.get("members") == pop.n:
+        if pmc.get("kernel_regex") and pmc["kernel_regex"] in kname and pmc.get("members") == pop.n:
             traffic = pmc["traffic_bytes_per_launch"]
 
     result = {
