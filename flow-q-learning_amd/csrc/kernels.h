@@ -28,7 +28,7 @@ inline TRef tref(float* p, long long ss, long long sy = 0) { return TRef{p, ss, 
 //   A(i,r) = A_RC ? A[i*lda + r] : A[r*lda + i]
 //   B(r,j) = B_RC ? B[j*ldb + r] : B[r*ldb + j]
 enum GemmLayout { LAYOUT_FWD = 0, LAYOUT_DX = 1, LAYOUT_DW = 2 };
-enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU2 = 2, EPI_BIAS_GELU = 3 };
+enum GemmEpi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU2 = 2, EPI_BIAS_GELU = 3, EPI_ADAM = 4 };
 
 struct GemmArgs {
     TRef A, B, C, C2, bias;
@@ -51,12 +51,36 @@ void launch_gemm_variant(int layout, int epi, int tile, int variant, const GemmA
 // Up to GEMM_GROUP_MAX independent dW-layout problems (A and B both
 // r-contiguous, EPI_STORE) in one launch; N % BN == 0 for every problem.
 constexpr int GEMM_GROUP_MAX = 8;
+// Fused optimiser epilogue of the grouped dW launch: problem gi is the kernel
+// leaf W_l of one net; its output tile is the gradient, and the epilogue runs
+// optax.adam on it (reading p from p_in, writing p_out, m, v in place), the
+// target-critic EMA from the pre-update value (critic only), the W_l^T copy
+// the streamed backward reads (hidden layers), and the tile's grad stats
+// (max, min, sum g^2) at chunk id stat_base[gi] + y * tiles_per_problem + tile.
+struct AdamEpi {
+    const float* p_in;
+    float *p_out, *m, *v, *target, *wt_out;
+    long long P, PT, PTT;             // slot strides of params / target / W^T arenas
+    long long ens, wt_sy;             // ensemble strides in params and W^T
+    long long w_off[GEMM_GROUP_MAX];  // leaf offset inside a params slot (net offset included)
+    long long wt_off[GEMM_GROUP_MAX]; // offset inside a W^T slot, -1 = no copy
+    int stat_base[GEMM_GROUP_MAX];
+    float* stats;                     // [slots][n_total_chunks][3]
+    int n_total_chunks;
+    const int* count;
+    float lr, tau;
+};
 struct GemmGroupArgs {
     GemmArgs g[GEMM_GROUP_MAX];
     int first[GEMM_GROUP_MAX + 1];   // prefix of per-problem block counts
     int ng;
+    AdamEpi adam;                    // used by the fused-Adam launch only
 };
-void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s);
+// tile: 2 = 64x128, 3 = 128x128 (others 64x64 / 128x64); adam != null: fused
+// optimiser epilogue (tile 2 or 3 only), else plain stores into g[i].C
+void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, const AdamEpi* adam = nullptr);
+// tiles per problem of the grouped dW launch (stats chunks of a fused W leaf)
+int gemm_group_tiles(int tile, int M, int N);
 
 // --------------------------------------------------- persistent Euler flow --
 // Euler steps first..S-1 of the BC flow (compute_flow_actions) for every active
@@ -273,12 +297,15 @@ void launch_loss_actor(const LossArgs& a, hipStream_t s);
 // ---------------------------------------------------------- optimiser ----
 struct Chunk { long long off; int len; int leaf; };  // element offset into a net's param block
 struct AdamArgs {
-    float *p, *g, *m, *v;         // arenas (slot stride P)
+    const float* p_in;            // parameters read (current buffer, slot stride P)
+    float* p_out;                 // parameters written (the other buffer of the pair)
+    float *g, *m, *v;             // arenas (slot stride P)
     float* target;                // target arena (slot stride PT) or null
     long long P, PT;
     long long net_off;            // offset of this net inside the params arena
-    const Chunk* chunks;          // chunk table of this net
-    int n_chunks, chunk_base;     // chunk ids chunk_base.. in the stats slab
+    const Chunk* chunks;          // chunk table of ALL nets (index = stats chunk id)
+    const int* ids;               // chunk ids to process (block = ids[blockIdx.x]), or null:
+    int n_chunks, chunk_base;     //   chunk ids chunk_base .. chunk_base + n_chunks - 1
     float* stats;                 // [slots][n_total_chunks][3] (max, min, sumsq)
     int n_total_chunks;
     const int* count;

@@ -154,9 +154,118 @@ constexpr int gemm_smem_floats() {
     return 2 * ((ARC ? BM * (BK + 1) : BK * BM) + (BRC ? BN * (BK + 1) : BK * BN)) + BM;
 }
 
+// Fused optimiser epilogue of a dW tile (AdamEpi in kernels.h).  The gradient
+// tile goes from the accumulators to LDS (the operand buffers are free after
+// the k-loop), then the block walks it in row order with float4 accesses:
+// optax.adam (b1 .9, b2 .999, eps 1e-8 outside the sqrt, bias correction with
+// count+1) reading p from the current buffer and writing the other one, the
+// target EMA from the pre-update p (critic), grad stats.  The new p goes back
+// into the LDS tile, and a second pass writes W^T rows (float4 along i).
+template <int BM, int BN, bool DUAL>
+DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc)[BM / 64][BN / 64],
+                       f32x16 (&acc2)[BM / 64][BN / 64], int slot, int y, int tile, int per, int i0, int j0,
+                       int wi, int wj, int l32, int lh, float* smem) {
+    constexpr int TM = BM / 64, TN = BN / 64;
+    constexpr int PT = BN + 1;  // LDS row pitch (odd: the transposed read of pass 2 spreads over banks)
+    static_assert(BM * PT <= gemm_smem_floats<BM, BN, 32, true, true>(), "gradient tile must fit the operand LDS");
+    const int gM = g.M, ldc = g.ldc, tid = threadIdx.x;
+    __syncthreads();  // every wave is done with the operand buffers
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            if constexpr (DUAL) acc[a][b] += acc2[a][b];
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                smem[(wi + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * PT + wj + b * 32 + l32] = acc[a][b][r];
+        }
+    __syncthreads();
+
+    const long long pb = (long long)slot * e.P + e.w_off[gi] + (long long)y * e.ens;
+    const float* __restrict__ Pi = e.p_in + pb;
+    float* __restrict__ Po = e.p_out + pb;
+    float* __restrict__ Mm = e.m + pb;
+    float* __restrict__ Vv = e.v + pb;
+    // the target arena mirrors the critic block, which sits at arena offset 0
+    float* __restrict__ Tt = e.target ? e.target + (long long)slot * e.PT + e.w_off[gi] + (long long)y * e.ens : nullptr;
+    const float t = (float)(e.count[slot] + 1);
+    const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
+    const float lr = e.lr, tau = e.tau;
+    float mx = -INFINITY, mn = INFINITY, ss = 0.f;
+    const int rows = min(BM, gM - i0);
+    // pass 1: thread -> 4 consecutive columns of a row; U iterations in flight
+    constexpr int TPR = BN / 4, RPI = 256 / TPR, U = 4;  // threads per row, rows per iteration
+    const int cj = (tid % TPR) * 4, ri = tid / TPR;
+    for (int r0 = 0; r0 < BM; r0 += RPI * U) {
+        float4 p4[U], m4[U], v4[U], t4[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = r0 + u * RPI + ri;
+            if (i < rows) {
+                const long long o = (long long)(i0 + i) * ldc + j0 + cj;
+                p4[u] = *reinterpret_cast<const float4*>(Pi + o);
+                m4[u] = *reinterpret_cast<const float4*>(Mm + o);
+                v4[u] = *reinterpret_cast<const float4*>(Vv + o);
+                if (Tt) t4[u] = *reinterpret_cast<const float4*>(Tt + o);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = r0 + u * RPI + ri;
+            if (i < rows) {
+                const long long o = (long long)(i0 + i) * ldc + j0 + cj;
+                float* gs = smem + i * PT + cj;
+                float pp[4] = {p4[u].x, p4[u].y, p4[u].z, p4[u].w};
+                float mm[4] = {m4[u].x, m4[u].y, m4[u].z, m4[u].w};
+                float vv[4] = {v4[u].x, v4[u].y, v4[u].z, v4[u].w};
+                float tt[4] = {t4[u].x, t4[u].y, t4[u].z, t4[u].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float gr = gs[c];
+                    mm[c] = 0.1f * gr + 0.9f * mm[c];
+                    vv[c] = 0.001f * (gr * gr) + 0.999f * vv[c];
+                    const float mh = mm[c] / bc1, vh = vv[c] / bc2;
+                    tt[c] = tau * pp[c] + (1.0f - tau) * tt[c];
+                    pp[c] = pp[c] + (-lr) * (mh / (sqrtf(vh) + 1e-8f));
+                    gs[c] = pp[c];
+                    mx = fmaxf(mx, gr);
+                    mn = fminf(mn, gr);
+                    ss += gr * gr;
+                }
+                *reinterpret_cast<float4*>(Po + o) = float4{pp[0], pp[1], pp[2], pp[3]};
+                *reinterpret_cast<float4*>(Mm + o) = float4{mm[0], mm[1], mm[2], mm[3]};
+                *reinterpret_cast<float4*>(Vv + o) = float4{vv[0], vv[1], vv[2], vv[3]};
+                if (Tt) *reinterpret_cast<float4*>(Tt + o) = float4{tt[0], tt[1], tt[2], tt[3]};
+            }
+        }
+    }
+    __shared__ float red[4];
+    mx = block_max(mx, red);  // (its barriers also publish the new p in LDS)
+    mn = block_min(mn, red);
+    ss = block_sum(ss, red);
+    if (tid == 0) {
+        float* st = e.stats + ((long long)slot * e.n_total_chunks + e.stat_base[gi] + y * per + tile) * 3;
+        st[0] = mx;
+        st[1] = mn;
+        st[2] = ss;
+    }
+    // pass 2 (hidden layers: M = H, full tiles): W^T[j][i0 .. i0+BM) as float4 runs along i
+    if (e.wt_off[gi] >= 0) {
+        float* __restrict__ WT = e.wt_out + (long long)slot * e.PTT + e.wt_off[gi] + (long long)y * e.wt_sy;
+        constexpr int TPC = BM / 4;  // threads per W^T row segment
+#pragma unroll 4
+        for (int q = tid; q < BM * BN / 4; q += 256) {
+            const int jj = q / TPC, ii = (q % TPC) * 4;
+            const float* src = smem + ii * PT + jj;
+            *reinterpret_cast<float4*>(WT + (long long)(j0 + jj) * gM + i0 + ii) =
+                float4{src[0], src[PT], src[2 * PT], src[3 * PT]};
+        }
+    }
+}
+
 // One output tile (logical block id w of the problem g) of the register-staged GEMM.
 template <int BM, int BN, int BK, bool DUAL, bool ARC, bool BRC, int EPI>
-DEV void gemm_body(const GemmArgs& g, int w, float* smem) {
+DEV void gemm_body(const GemmArgs& g, int w, float* smem, const AdamEpi* ae = nullptr, int gi = 0) {
     constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
     constexpr int A_SZ = ARC ? BM * (BK + 1) : BK * BM;
     constexpr int B_SZ = BRC ? BN * (BK + 1) : BK * BN;
@@ -180,7 +289,7 @@ DEV void gemm_body(const GemmArgs& g, int w, float* smem) {
     float* As1 = smem + A_SZ + B_SZ;
     float* Bs1 = As1 + A_SZ;
     float* bias_s = smem + 2 * (A_SZ + B_SZ);
-    if constexpr (EPI != EPI_STORE) {
+    if constexpr (EPI != EPI_STORE && EPI != EPI_ADAM) {
         if (threadIdx.x < BM) {
             const int i = i0 + threadIdx.x;
             bias_s[threadIdx.x] = i < gM ? at(g.bias, slot, y)[i] : 0.f;
@@ -264,6 +373,10 @@ DEV void gemm_body(const GemmArgs& g, int w, float* smem) {
 
     // epilogue: accumulator register r of a 32x32 tile holds
     // row i = (r&3) + 8*(r>>2) + 4*(lane>>5), column j = lane&31.
+    if constexpr (EPI == EPI_ADAM) {
+        adam_epilogue<BM, BN, DUAL>(*ae, gi, g, acc, acc2, slot, y, tile, per, i0, j0, wi, wj, l32, lh, smem);
+        return;
+    }
     float* __restrict__ C = at(g.C, slot, y);
     float* __restrict__ C2 = (EPI == EPI_BIAS_GELU2) ? at(g.C2, slot, y) : nullptr;
     const int ldc = g.ldc;
@@ -315,7 +428,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
 
 // Grouped launch of independent problems of one layout (the dW GEMMs of every
 // layer of a network): block -> problem by the prefix of tile counts.
-template <int BM, int BN, bool ARC, bool BRC>
+template <int BM, int BN, bool ARC, bool BRC, int EPI = EPI_STORE>
 __global__ __launch_bounds__(256, 2) void gemm_group_kernel(const GemmGroupArgs ga) {
     __shared__ __attribute__((aligned(16))) float smem[gemm_smem_floats<BM, BN, 32, ARC, BRC>()];
     const int bid = xcd_remap(blockIdx.x, ga.first[ga.ng]);
@@ -323,20 +436,32 @@ __global__ __launch_bounds__(256, 2) void gemm_group_kernel(const GemmGroupArgs 
 #pragma unroll
     for (int i = 1; i < GEMM_GROUP_MAX; ++i)
         if (i < ga.ng && bid >= ga.first[i]) gi = i;
-    gemm_body<BM, BN, 32, false, ARC, BRC, EPI_STORE>(ga.g[gi], bid - ga.first[gi], smem);
+    gemm_body<BM, BN, 32, false, ARC, BRC, EPI>(ga.g[gi], bid - ga.first[gi], smem, &ga.adam, gi);
 }
 
-void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s) {
-    GemmGroupArgs ga{};
+int gemm_group_tiles(int tile, int M, int N) {
     const int bm = (tile & 1) ? 128 : 64, bn = (tile & 2) ? 128 : 64;
+    return ((M + bm - 1) / bm) * (N / bn);
+}
+
+void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, const AdamEpi* adam) {
+    GemmGroupArgs ga{};
     int tot = 0;
     for (int i = 0; i < ng; ++i) {
         ga.g[i] = gs[i];
         ga.first[i] = tot;
-        tot += ((gs[i].M + bm - 1) / bm) * (gs[i].N / bn) * gs[i].ny * gs[i].nz;
+        tot += gemm_group_tiles(tile, gs[i].M, gs[i].N) * gs[i].ny * gs[i].nz;
     }
     ga.first[ng] = tot;
     ga.ng = ng;
+    if (adam) {
+        ga.adam = *adam;
+        if (tile == 3)
+            hipLaunchKernelGGL((gemm_group_kernel<128, 128, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga);
+        else
+            hipLaunchKernelGGL((gemm_group_kernel<64, 128, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga);
+        return;
+    }
     switch (tile) {
         case 0: hipLaunchKernelGGL((gemm_group_kernel<64, 64, true, true>), dim3(tot), dim3(256), 0, s, ga); break;
         case 1: hipLaunchKernelGGL((gemm_group_kernel<128, 64, true, true>), dim3(tot), dim3(256), 0, s, ga); break;
@@ -1963,11 +2088,12 @@ void launch_loss_actor(const LossArgs& a, hipStream_t s) {
 // with count+1) fused with the target-critic EMA (from the PRE-update critic)
 // and the per-chunk grad statistics of apply_loss_fn (max, min, sum g^2).
 __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
-    const int ci = blockIdx.x, z = blockIdx.y;
+    const int ci = a.ids ? a.ids[blockIdx.x] : a.chunk_base + blockIdx.x, z = blockIdx.y;
     const int slot = a.slots[z];
     const Chunk ck = a.chunks[ci];
     const long long base = (long long)slot * a.P + a.net_off + ck.off;
-    float* __restrict__ P = a.p + base;
+    const float* __restrict__ Pin = a.p_in + base;
+    float* __restrict__ P = a.p_out + base;
     const float* __restrict__ G = a.g + base;
     float* __restrict__ Mm = a.m + base;
     float* __restrict__ V = a.v + base;
@@ -1992,7 +2118,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     if ((ck.len & 3) == 0) {
         for (int i = threadIdx.x * 4; i < ck.len; i += 1024) {
             const float4 g4 = *reinterpret_cast<const float4*>(G + i);
-            float4 p4 = *reinterpret_cast<float4*>(P + i);
+            float4 p4 = *reinterpret_cast<const float4*>(Pin + i);
             float4 m4 = *reinterpret_cast<float4*>(Mm + i);
             float4 v4 = *reinterpret_cast<float4*>(V + i);
             float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2009,7 +2135,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     } else {
         for (int i = threadIdx.x; i < ck.len; i += 256) {
             const float gv = G[i];
-            float p = P[i], m = Mm[i], v = V[i], tv = hasT ? T[i] : 0.f;
+            float p = Pin[i], m = Mm[i], v = V[i], tv = hasT ? T[i] : 0.f;
             FQ_ADAM1(gv, p, m, v, hasT, tv);
             P[i] = p;
             Mm[i] = m;
@@ -2023,7 +2149,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
     mn = block_min(mn, red);
     ss = block_sum(ss, red);
     if (threadIdx.x == 0) {
-        float* st = a.stats + ((long long)slot * a.n_total_chunks + a.chunk_base + ci) * 3;
+        float* st = a.stats + ((long long)slot * a.n_total_chunks + ci) * 3;
         st[0] = mx;
         st[1] = mn;
         st[2] = ss;

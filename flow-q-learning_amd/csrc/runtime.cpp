@@ -123,7 +123,15 @@ struct fqlpop {
     long long state_size = 0;
 
     // device state
-    float *params = nullptr, *grads = nullptr, *adam_m = nullptr, *adam_v = nullptr, *target = nullptr;
+    // Parameters are double-buffered: a step reads every parameter from
+    // `params` and its optimiser writes `params_nx`; the host swaps the pair
+    // after enqueueing a train step (flip_params).  So no kernel of a step has
+    // to wait for another's last read of a parameter before updating it.
+    float* params_buf[2] = {nullptr, nullptr};
+    float* paramsT_buf[2] = {nullptr, nullptr};
+    int cur = 0;
+    float *params = nullptr, *params_nx = nullptr;
+    float *grads = nullptr, *adam_m = nullptr, *adam_v = nullptr, *target = nullptr;
     int* count = nullptr;
     uint64_t* seeds = nullptr;
     float* alpha = nullptr;
@@ -133,6 +141,12 @@ struct fqlpop {
     int* chunk_leaf = nullptr;
     int* leaf_first = nullptr;
     int n_chunks_net[3] = {0, 0, 0}, chunk_base_net[3] = {0, 0, 0}, n_chunks_total = 0;
+    // fused optimiser (Adam in the dW epilogue): stats chunk id of each net's
+    // W_l tiles, and the remaining (small-leaf) chunks the adam kernel runs
+    bool fused_adam = false;
+    int w_stat_base[3][EF_MAX_LAYERS] = {};
+    int* res_ids = nullptr;
+    int res_base[3] = {0, 0, 0}, res_n[3] = {0, 0, 0};
     int n_train_leaves = 0;
 
     // host mirror
@@ -172,7 +186,7 @@ struct fqlpop {
     float *part_cr = nullptr, *part_bc = nullptr, *part_os = nullptr;  // stream_bwd column-sum partials
     // W_l^T copies of the hidden kernels (l = 1..L-1) for stream_bwd, per slot:
     // [critic e=0..E-1 | bc | os] x (L-1) x H x H; refreshed after each Adam
-    float* paramsT = nullptr;
+    float *paramsT = nullptr, *paramsT_nx = nullptr;   // current / next buffer (see params)
     long long PTT = 0, wt_net_off[3] = {0, 0, 0};
     bool wt_dirty = true;          // params changed on the host side: re-transpose before the next step
     // world-model rollout evaluator (fqlpop_set_env_model / fqlpop_rollout)
@@ -193,7 +207,7 @@ struct fqlpop {
     double probe_total_ms = 0.0;
     long long probe_launches = 0;
     double clock_check_event_us = 0.0, clock_check_stamp_us = 0.0;
-    std::map<int, Graphs> graphs;  // key: train*2 + injected
+    std::map<long long, Graphs> graphs;  // key: mode, active count, probe set, current buffer
 
     float* alloc(long long per_slot) {
         float* p = nullptr;
@@ -266,18 +280,33 @@ long long leaf_member_size(const NetLayout& N, int kind, int layer) {
     return N.H;
 }
 
+// dW group tile of a net (stream_bwd_net): 128x128 for the 2-ensemble critic
+int dw_tile(const NetLayout& N) { return N.E > 1 ? 3 : 2; }
+
 void build_chunks(fqlpop* h) {
     constexpr int CH = 16384;
     std::vector<Chunk> all;
-    std::vector<int> all_leaf;
+    std::vector<int> all_leaf, res;
     const NetLayout* nets[3] = {&h->critic, &h->bc, &h->os};
     int leaf_id = 0;
     for (int ni = 0; ni < 3; ++ni) {
         const NetLayout& N = *nets[ni];
         h->chunk_base_net[ni] = (int)all.size();
+        h->res_base[ni] = (int)res.size();
         for (int l = 0; l <= N.L; ++l) {
             for (int kind = 0; kind < 4; ++kind) {
                 if (kind >= 2 && (l == N.L || !N.ln)) continue;
+                if (h->fused_adam && kind == 0 && l < N.L) {
+                    // W_l: the fused dW epilogue writes one stats chunk per tile
+                    h->w_stat_base[ni][l] = (int)all.size();
+                    const int nt = gemm_group_tiles(dw_tile(N), N.kdim(l), N.H) * N.E;
+                    for (int t = 0; t < nt; ++t) {
+                        all.push_back(Chunk{0, 0, leaf_id});
+                        all_leaf.push_back(leaf_id);
+                    }
+                    ++leaf_id;
+                    continue;
+                }
                 const long long len = leaf_member_size(N, kind, l);
                 for (int e = 0; e < N.E; ++e) {
                     const long long base = e * N.ens_size + leaf_internal_off(N, kind, l);
@@ -286,6 +315,7 @@ void build_chunks(fqlpop* h) {
                         c.off = base + s;
                         c.len = (int)std::min<long long>(CH, len - s);
                         c.leaf = leaf_id;
+                        res.push_back((int)all.size());
                         all.push_back(c);
                         all_leaf.push_back(leaf_id);
                     }
@@ -294,7 +324,10 @@ void build_chunks(fqlpop* h) {
             }
         }
         h->n_chunks_net[ni] = (int)all.size() - h->chunk_base_net[ni];
+        h->res_n[ni] = (int)res.size() - h->res_base[ni];
     }
+    HIPCHK(hipMalloc(&h->res_ids, sizeof(int) * std::max<size_t>(1, res.size())));
+    if (!res.empty()) HIPCHK(hipMemcpy(h->res_ids, res.data(), sizeof(int) * res.size(), hipMemcpyHostToDevice));
     h->n_chunks_total = (int)all.size();
     h->n_train_leaves = leaf_id;
     ARGCHK(leaf_id <= 128, "too many leaves");
@@ -314,6 +347,14 @@ void build_chunks(fqlpop* h) {
 }
 
 // ------------------------------------------------------------- params init
+// Copy a slot's current parameters into the other buffer of the pair (after a
+// host-side write, or for a member that stops stepping: both buffers must hold
+// its parameters whichever one is current when it steps again).
+void mirror_params(fqlpop* h, int slot, hipStream_t s) {
+    HIPCHK(hipMemcpyAsync(h->params_nx + (long long)slot * h->P, h->params + (long long)slot * h->P,
+                          sizeof(float) * h->P, hipMemcpyDeviceToDevice, s));
+}
+
 void init_member(fqlpop* h, int slot, uint64_t seed) {
     unsigned salt = 1;
     auto init_net = [&](const NetLayout& N) {
@@ -343,6 +384,7 @@ void init_member(fqlpop* h, int slot, uint64_t seed) {
     HIPCHK(hipMemcpyAsync(h->target + (long long)slot * h->PT, h->params + (long long)slot * h->P,
                           sizeof(float) * h->PT, hipMemcpyDeviceToDevice, h->sM));
     HIPCHK(hipMemsetAsync(h->count + slot, 0, sizeof(int), h->sM));
+    mirror_params(h, slot, h->sM);
     HIPCHK(hipStreamSynchronize(h->sM));
     h->wt_dirty = true;
 }
@@ -587,19 +629,39 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         gw.ny = N.E; gw.nz = c.nz; gw.slots = h->slots;
         gs.push_back(gw);
     }
-    if (N.L <= GEMM_GROUP_MAX && N.H % 128 == 0) {
-        launch_gemm_group_dw(N.E > 1 ? 3 : 2, gs.data(), (int)gs.size(), sw);
+    if (h->fused_adam) {
+        // dW of every layer with Adam / EMA / W^T / grad stats in the epilogue
+        AdamEpi ae{};
+        ae.p_in = h->params; ae.p_out = h->params_nx; ae.m = h->adam_m; ae.v = h->adam_v;
+        ae.target = ni == 0 ? h->target : nullptr;
+        ae.wt_out = h->paramsT_nx;
+        ae.P = h->P; ae.PT = h->PT; ae.PTT = h->PTT;
+        ae.ens = N.ens_size;
+        ae.wt_sy = (long long)(N.L - 1) * N.H * N.H;
+        for (int gi = 0; gi < (int)gs.size(); ++gi) {
+            const int l = N.L - 1 - gi;
+            ae.w_off[gi] = N.off + N.W[l];
+            ae.wt_off[gi] = l >= 1 ? h->wt_net_off[ni] + (long long)(l - 1) * N.H * N.H : -1;
+            ae.stat_base[gi] = h->w_stat_base[ni][l];
+        }
+        ae.stats = h->stats; ae.n_total_chunks = h->n_chunks_total;
+        ae.count = h->count;
+        ae.lr = h->cfg.lr; ae.tau = h->cfg.tau;
+        launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw, &ae);
+    } else if (N.L <= GEMM_GROUP_MAX && N.H % 128 == 0) {
+        launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw);
     } else {
         for (const GemmArgs& gw : gs) gemm(LAYOUT_DW, EPI_STORE, gw, sw);
     }
 }
 
-// Refresh the W^T copies of the nets in `mask` (bit ni: 0 critic, 1 bc, 2 os)
-// for the active slots (all slots when all_slots).
-void transpose_nets(fqlpop* h, hipStream_t s, int mask, bool all_slots) {
+// W^T copies (dst, a paramsT buffer) of the hidden kernels of the nets in
+// `mask` (bit ni: 0 critic, 1 bc, 2 os) from src (a params buffer), for the
+// active slots (all slots when all_slots).
+void transpose_nets(fqlpop* h, hipStream_t s, int mask, bool all_slots, const float* src, float* dst) {
     TransposeArgs t{};
-    t.src = h->params; t.src_ss = h->P;
-    t.dst = h->paramsT; t.dst_ss = h->PTT;
+    t.src = src; t.src_ss = h->P;
+    t.dst = dst; t.dst_ss = h->PTT;
     t.H = h->H;
     const NetLayout* nets[3] = {&h->critic, &h->bc, &h->os};
     const long long HH = (long long)h->H * h->H;
@@ -621,17 +683,27 @@ void transpose_nets(fqlpop* h, hipStream_t s, int mask, bool all_slots) {
     launch_transpose(t, s);
 }
 
+// Adam (+ EMA, grad stats) of net ni from params to params_nx: every leaf, or
+// with the fused optimiser only the leaves the dW epilogue does not cover.
 void adam_net(const Ctx& c, hipStream_t s, int ni) {
     fqlpop* h = c.h;
     const NetLayout* nets[3] = {&h->critic, &h->bc, &h->os};
     AdamArgs a{};
-    a.p = h->params; a.g = h->grads; a.m = h->adam_m; a.v = h->adam_v;
+    a.p_in = h->params; a.p_out = h->params_nx;
+    a.g = h->grads; a.m = h->adam_m; a.v = h->adam_v;
     a.target = ni == 0 ? h->target : nullptr;
     a.P = h->P; a.PT = h->PT;
     a.net_off = nets[ni]->off;
-    a.chunks = h->chunks + h->chunk_base_net[ni];
-    a.n_chunks = h->n_chunks_net[ni];
-    a.chunk_base = h->chunk_base_net[ni];
+    a.chunks = h->chunks;
+    if (h->fused_adam) {
+        a.ids = h->res_ids + h->res_base[ni];
+        a.n_chunks = h->res_n[ni];
+    } else {
+        a.ids = nullptr;
+        a.n_chunks = h->n_chunks_net[ni];
+        a.chunk_base = h->chunk_base_net[ni];
+    }
+    if (a.n_chunks == 0) return;
     a.stats = h->stats; a.n_total_chunks = h->n_chunks_total;
     a.count = h->count;
     a.lr = h->cfg.lr; a.tau = h->cfg.tau;
@@ -813,7 +885,8 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         HIPCHK(hipStreamWaitEvent(to, ev, 0));
     };
 
-    // ---- sB: BC loss + backward (+ Adam after the flow chain) ------------
+    // ---- sB: BC loss + backward + Adam ------------------------------------
+    // (Adam writes params_nx, so it need not wait for the flow's reads)
     HIPCHK(hipStreamWaitEvent(sB, h->ev_bcfwd, 0));
     launch_loss_bc(la, sB);
     HIPCHK(hipEventRecord(h->ev_bcloss, sB));
@@ -825,9 +898,8 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         else
             bwd_net(c, sB, N, tref(h->dv, (long long)A * B), B, tref(h->bc_in, (long long)Kb * B2), B2, 0, B, B,
                     h->bc_u, h->bc_g, 0, nullptr, nullptr, 0, h->bc_du, h->bc_dh, nullptr, nullptr, B, sB);
-        HIPCHK(hipStreamWaitEvent(sB, h->ev_flow, 0));  // Euler reads bc params
         adam_net(c, sB, 1);
-        if (h->stream_bwd) transpose_nets(h, sB, 2, false);
+        if (h->stream_bwd && !h->fused_adam) transpose_nets(h, sB, 2, false, h->params_nx, h->paramsT_nx);
     }
     HIPCHK(hipEventRecord(h->ev_bdone, sB));
 
@@ -925,10 +997,11 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         ig.H = H; ig.D = D; ig.A = A; ig.E = E; ig.ld = B2; ig.off = B; ig.M = B;
         ig.nz = c.nz; ig.slots = h->slots;
         launch_input_grad(ig, sM);
-        // critic Adam + target EMA once every read of the critic params is done
-        dep(sM, sX);
+        // critic Adam + target EMA (the fused dW launch already covered the
+        // kernels); the per-layer backward writes grads on sM too: join it
+        if (!h->fused_adam) dep(sM, sX);
         adam_net(c, sX, 0);
-        if (h->stream_bwd) transpose_nets(h, sX, 1, false);
+        if (h->stream_bwd && !h->fused_adam) transpose_nets(h, sX, 1, false, h->params_nx, h->paramsT_nx);
     }
     HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
     HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
@@ -941,9 +1014,9 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         else
             bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3, B, B,
                     B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, h->os_dh, nullptr, nullptr, B, sX);
-        dep(sM, sX);
+        if (!h->fused_adam) dep(sM, sX);
         adam_net(c, sX, 2);
-        if (h->stream_bwd) transpose_nets(h, sX, 4, false);
+        if (h->stream_bwd && !h->fused_adam) transpose_nets(h, sX, 4, false, h->params_nx, h->paramsT_nx);
         dep(sX, sM);
         HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
         FinalArgs fa{};
@@ -959,20 +1032,31 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     HIPCHK(hipGetLastError());
 }
 
+// Swap the parameter buffer pairs after a train step was enqueued.
+void flip_params(fqlpop* h) {
+    h->cur ^= 1;
+    h->params = h->params_buf[h->cur];
+    h->params_nx = h->params_buf[h->cur ^ 1];
+    h->paramsT = h->paramsT_buf[h->cur];
+    h->paramsT_nx = h->paramsT_buf[h->cur ^ 1];
+}
+
 void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     if (h->nz == 0) return;
-    if (train && h->stream_bwd && h->wt_dirty) {  // params set on the host side since the last step
-        transpose_nets(h, h->sM, 7, true);
+    if (h->stream_bwd && h->wt_dirty) {  // params set on the host side since the last step
+        transpose_nets(h, h->sM, 7, true, h->params, h->paramsT);
+        transpose_nets(h, h->sM, 7, true, h->params, h->paramsT_nx);
         h->wt_dirty = false;
     }
     if (!h->cfg.use_graph) {
         enqueue(h, train, inj_batch, inj_noise);
+        if (train) flip_params(h);
         return;
     }
     // one graph per (mode, active-member count): kernels read the active slot ids
     // from device memory, so any active set of the same size replays the graph
-    const int key = ((train ? 4 : 0) + (inj_batch ? 2 : 0) + (inj_noise ? 1 : 0)) + 8 * h->nz +
-                    (1 << 20) * (h->probe_set + 1);
+    const long long key = ((train ? 4 : 0) + (inj_batch ? 2 : 0) + (inj_noise ? 1 : 0)) + 8LL * h->nz +
+                          (1LL << 32) * (h->probe_set + 1) + (1LL << 36) * h->cur;
     Graphs& gr = h->graphs[key];
     if (gr.exec == nullptr || gr.nz != h->nz) {
         if (gr.exec) HIPCHK(hipGraphExecDestroy(gr.exec));
@@ -991,6 +1075,7 @@ void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         gr.nz = h->nz;
     }
     HIPCHK(hipGraphLaunch(gr.exec, h->sM));
+    if (train) flip_params(h);
 }
 
 // Launch duration from per-block stamps: max(end) - min(start) over the blocks
@@ -1152,6 +1237,12 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             h->stream_bwd = stream_bwd_supported(H, L, A, B, B) &&
                             !(sb && std::atoi(sb) == 0);
         }
+        {
+            // Adam / EMA / W^T / grad stats fused into the grouped dW epilogue
+            const char* fa = std::getenv("FQLPOP_FUSED_ADAM");
+            h->fused_adam = h->stream_bwd && H % 128 == 0 && L <= GEMM_GROUP_MAX && h->critic.off == 0 &&
+                            !(fa && std::atoi(fa) == 0);
+        }
         if (h->euler_fused) {  // dominant kernel: one persistent Euler launch per step
             h->probe_pairs = 1;
             h->probe_blocks = (long long)(cfg->batch_size / 16) * n_members;
@@ -1170,12 +1261,16 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         HIPCHK(hipEventCreate(&h->ev_t1));
 
         const int n = h->n;
-        HIPCHK(hipMalloc(&h->params, sizeof(float) * h->P * n));
+        for (float*& pb : h->params_buf) {
+            HIPCHK(hipMalloc(&pb, sizeof(float) * h->P * n));
+            HIPCHK(hipMemset(pb, 0, sizeof(float) * h->P * n));
+        }
+        h->params = h->params_buf[0];
+        h->params_nx = h->params_buf[1];
         HIPCHK(hipMalloc(&h->grads, sizeof(float) * h->P * n));
         HIPCHK(hipMalloc(&h->adam_m, sizeof(float) * h->P * n));
         HIPCHK(hipMalloc(&h->adam_v, sizeof(float) * h->P * n));
         HIPCHK(hipMalloc(&h->target, sizeof(float) * h->PT * n));
-        HIPCHK(hipMemset(h->params, 0, sizeof(float) * h->P * n));
         HIPCHK(hipMemset(h->grads, 0, sizeof(float) * h->P * n));
         HIPCHK(hipMalloc(&h->count, sizeof(int) * n));
         HIPCHK(hipMalloc(&h->seeds, sizeof(uint64_t) * n));
@@ -1217,7 +1312,8 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             h->wt_net_off[1] = (long long)E * (L - 1) * HH;
             h->wt_net_off[2] = (long long)(E + 1) * (L - 1) * HH;
             h->PTT = (long long)(E + 2) * (L - 1) * HH;
-            h->paramsT = h->alloc(std::max<long long>(1, h->PTT));
+            h->paramsT_buf[0] = h->paramsT = h->alloc(std::max<long long>(1, h->PTT));
+            h->paramsT_buf[1] = h->paramsT_nx = h->alloc(std::max<long long>(1, h->PTT));
         }
         h->cr_dh = h->alloc((long long)H * B2 * E);
         h->bc_dh = h->alloc((long long)H * B);
@@ -1259,7 +1355,7 @@ int fqlpop_destroy(fqlpop_t* h) {
         for (auto& kv : h->graphs)
             if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
         for (float* p : h->allocs) (void)hipFree(p);
-        for (void* p : {(void*)h->params, (void*)h->grads, (void*)h->adam_m, (void*)h->adam_v, (void*)h->target,
+        for (void* p : {(void*)h->params_buf[0], (void*)h->params_buf[1], (void*)h->res_ids, (void*)h->grads, (void*)h->adam_m, (void*)h->adam_v, (void*)h->target,
                         (void*)h->count, (void*)h->seeds, (void*)h->alpha, (void*)h->slots, (void*)h->stats,
                         (void*)h->chunks, (void*)h->chunk_leaf, (void*)h->leaf_first, (void*)h->sp_params,
                         (void*)h->tp_params})
@@ -1316,6 +1412,11 @@ int fqlpop_set_active(fqlpop_t* h, const uint8_t* mask) {
         ARGCHK(h && mask, "null argument");
         for (int i = 0; i < h->n; ++i) h->active[i] = mask[i] ? 1 : 0;
         update_slots(h);
+        // a member that does not step keeps its parameters in both buffers
+        for (int i = 0; i < h->n; ++i)
+            if (!h->active[i]) mirror_params(h, i, h->sM);
+        HIPCHK(hipStreamSynchronize(h->sM));
+        h->wt_dirty = true;
     });
 }
 
@@ -1493,9 +1594,12 @@ static void state_copy(fqlpop* h, int member, int which, float* flat, const floa
     if (!get) {
         if (which == 0) h->wt_dirty = true;
         HIPCHK(hipMemcpy(arena + (long long)member * h->P, blk.data(), sizeof(float) * h->P, hipMemcpyHostToDevice));
-        if (which == 0)
+        if (which == 0) {
             HIPCHK(hipMemcpy(h->target + (long long)member * h->PT, tblk.data(), sizeof(float) * h->PT,
                              hipMemcpyHostToDevice));
+            mirror_params(h, member, h->sM);
+            HIPCHK(hipStreamSynchronize(h->sM));
+        }
     }
 }
 
