@@ -456,10 +456,12 @@ void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, c
     ga.ng = ng;
     if (adam) {
         ga.adam = *adam;
-        if (tile == 3)
-            hipLaunchKernelGGL((gemm_group_kernel<128, 128, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga);
-        else
-            hipLaunchKernelGGL((gemm_group_kernel<64, 128, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga);
+        switch (tile) {
+            case 0: hipLaunchKernelGGL((gemm_group_kernel<64, 64, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga); break;
+            case 1: hipLaunchKernelGGL((gemm_group_kernel<128, 64, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga); break;
+            case 2: hipLaunchKernelGGL((gemm_group_kernel<64, 128, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga); break;
+            default: hipLaunchKernelGGL((gemm_group_kernel<128, 128, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga); break;
+        }
         return;
     }
     switch (tile) {

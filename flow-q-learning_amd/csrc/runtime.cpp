@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -280,8 +281,15 @@ long long leaf_member_size(const NetLayout& N, int kind, int layer) {
     return N.H;
 }
 
-// dW group tile of a net (stream_bwd_net): 128x128 for the 2-ensemble critic
-int dw_tile(const NetLayout& N) { return N.E > 1 ? 3 : 2; }
+// dW group tile of a net (stream_bwd_net; 0 = 64x64, 1 = 128x64, 2 = 64x128, 3 = 128x128)
+// (64 x 128 for every net: with the fused optimiser epilogue, 3 blocks per CU
+// overlap one block's HBM-bound epilogue with the others' k-loops better than
+// 2 blocks of 128 x 128; FQLPOP_DW_TILE_C / _A override, for measurements)
+int dw_tile(const NetLayout& N) {
+    const char* t = std::getenv(N.E > 1 ? "FQLPOP_DW_TILE_C" : "FQLPOP_DW_TILE_A");
+    if (t) return std::atoi(t);
+    return 2;
+}
 
 void build_chunks(fqlpop* h) {
     constexpr int CH = 16384;
@@ -566,7 +574,8 @@ void bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_
 void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_o, TRef X0, int ld,
                     long long coff, int M, int Mg, const std::vector<float*>& U, const std::vector<float*>& G,
                     long long act_sy, const std::vector<float*>* MU, const std::vector<float*>* RS, long long st_sy,
-                    const std::vector<float*>& DU, int ld_d, float* part, hipStream_t sw) {
+                    const std::vector<float*>& DU, int ld_d, float* part, hipStream_t sw,
+                    const InGradArgs* ig = nullptr, std::function<void()>* defer = nullptr) {
     fqlpop* h = c.h;
     const long long act_ss = (long long)N.H * ld * N.E;
     const long long d_ss = (long long)N.H * ld_d * N.E, d_sy = (long long)N.H * ld_d;
@@ -600,13 +609,21 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
     a.L = N.L; a.M = M; a.Mg = Mg; a.nout = N.out_dim;
     a.ny = N.E; a.nz = c.nz; a.slots = h->slots;
     launch_stream_bwd(N.ln, a, s);
+    // the critic's dQ/da goes first: the actor chain waits for it, not for the dW
+    if (ig) launch_input_grad(*ig, s);
+    hipEvent_t ev = nullptr;
     if (sw != s) {
-        hipEvent_t ev = next_event(h);
+        ev = next_event(h);
         HIPCHK(hipEventRecord(ev, s));
-        HIPCHK(hipStreamWaitEvent(sw, ev, 0));
     }
+    // the parameter-grad half (partial reduction + dW, fused optimiser): now,
+    // or by the caller later (`defer`), so that the step's critical chain is
+    // captured ahead of it
+    const int NP = a.NP;
+    auto dw_half = [=, &N]() {
+    if (ev) HIPCHK(hipStreamWaitEvent(sw, ev, 0));
     ColsumArgs r{};
-    r.part = part; r.NP = a.NP; r.tiles = Mg / 16;
+    r.part = part; r.NP = NP; r.tiles = Mg / 16;
     r.grads = h->grads + N.off; r.P = h->P; r.ens = N.ens_size;
     for (int l = 0; l < N.L; ++l) {
         r.b_off[l] = N.b[l];
@@ -653,6 +670,9 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
     } else {
         for (const GemmArgs& gw : gs) gemm(LAYOUT_DW, EPI_STORE, gw, sw);
     }
+    };
+    if (defer) *defer = dw_half;
+    else dw_half();
 }
 
 // W^T copies (dst, a paramsT buffer) of the hidden kernels of the nets in
@@ -981,42 +1001,61 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     }
     dep(sX, sM);  // Q_target
     launch_loss_critic(la, sM);
+    // fused optimiser: the critic's dW + Adam is captured after the actor's dX
+    // chain (it runs beside it instead of ahead of it on a shared queue)
+    std::function<void()> critic_dw;
     if (train) {
         // critic backward: the dX chain stays on sM, the dW GEMMs go to sX
-        if (h->stream_bwd)
-            stream_bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0),
-                           B2, 0, B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, B2, h->part_cr, sX);
-        else
-            bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0), B2, 0,
-                    B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, h->cr_dh, h->cr_c1, h->cr_c2,
-                    B2, sX);
         InGradArgs ig{};
         ig.W0 = pref(h, h->params, NC, NC.W[0]);
         ig.du0 = tref(h->cr_du[0], (long long)H * B2 * E, sy2);
         ig.da = tref(h->da, (long long)A * B);
         ig.H = H; ig.D = D; ig.A = A; ig.E = E; ig.ld = B2; ig.off = B; ig.M = B;
         ig.nz = c.nz; ig.slots = h->slots;
-        launch_input_grad(ig, sM);
-        // critic Adam + target EMA (the fused dW launch already covered the
-        // kernels); the per-layer backward writes grads on sM too: join it
-        if (!h->fused_adam) dep(sM, sX);
-        adam_net(c, sX, 0);
-        if (h->stream_bwd && !h->fused_adam) transpose_nets(h, sX, 1, false, h->params_nx, h->paramsT_nx);
+        if (h->stream_bwd) {
+            stream_bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0),
+                           B2, 0, B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, B2, h->part_cr, sX,
+                           &ig, h->fused_adam ? &critic_dw : nullptr);
+        } else {
+            bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0), B2, 0,
+                    B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, h->cr_dh, h->cr_c1, h->cr_c2,
+                    B2, sX);
+            launch_input_grad(ig, sM);
+        }
+        // critic Adam + target EMA; the per-layer backward writes grads on sM too: join it
+        if (!h->fused_adam) {
+            dep(sM, sX);
+            adam_net(c, sX, 0);
+            if (h->stream_bwd) transpose_nets(h, sX, 1, false, h->params_nx, h->paramsT_nx);
+        }
     }
     HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
     HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
     launch_loss_actor(la, sM);
     if (train) {
         const NetLayout& N = h->os;
-        if (h->stream_bwd)
+        if (h->fused_adam) {
+            // actor dX chain, then the critic's grads + Adam (sX) beside the
+            // actor's (sM), then the join
+            std::function<void()> os_dw;
+            stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3,
+                           B, B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, B, h->part_os, sM, nullptr,
+                           &os_dw);
+            critic_dw();
+            adam_net(c, sX, 0);
+            os_dw();
+            adam_net(c, sM, 2);
+        } else if (h->stream_bwd)
             stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3,
                            B, B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, B, h->part_os, sX);
         else
             bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3, B, B,
                     B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, h->os_dh, nullptr, nullptr, B, sX);
-        if (!h->fused_adam) dep(sM, sX);
-        adam_net(c, sX, 2);
-        if (h->stream_bwd && !h->fused_adam) transpose_nets(h, sX, 4, false, h->params_nx, h->paramsT_nx);
+        if (!h->fused_adam) {
+            dep(sM, sX);
+            adam_net(c, sX, 2);
+            if (h->stream_bwd) transpose_nets(h, sX, 4, false, h->params_nx, h->paramsT_nx);
+        }
         dep(sX, sM);
         HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
         FinalArgs fa{};

@@ -149,7 +149,7 @@ __global__ __launch_bounds__(512, 1) void mlp_stream_cg(const float* __restrict_
         const int f = e / NCT, j = e % NCT;
         slab[e] = X[((long long)m * H + f) * ncols + c0 + j];
     }
-    const rsrc_t rW = make_rsrc(W + (long long)m * LAYERS * H * H, (long long)LAYERS * H * H);
+    const rsrc_t rW = make_rsrc(W + (MODE == 5 ? 0LL : (long long)m) * LAYERS * H * H, (long long)LAYERS * H * H);
     const int lo = lk * H + 64 * w + 4 * li;
     constexpr int NS = H / 4;
     float4 ring[PF];
@@ -177,7 +177,9 @@ __global__ __launch_bounds__(512, 1) void mlp_stream_cg(const float* __restrict_
 #pragma unroll
                 for (int g = 0; g < CG; ++g) {
                     b[g] = bnext[g];
-                    bnext[g] = slab[(4 * (s + 1) + lk) * NCT + 16 * g + li];
+                    // MODE 3: no LDS reads either (MFMA issue ceiling of the structure)
+                    if (MODE >= 3) bnext[g] += 1e-9f;
+                    else bnext[g] = slab[(4 * (s + 1) + lk) * NCT + 16 * g + li];
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 const float4 a = ring[p];
@@ -191,10 +193,16 @@ __global__ __launch_bounds__(512, 1) void mlp_stream_cg(const float* __restrict_
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 // MODE 1: no weight loads (MFMA + LDS ceiling); MODE 2: loads only
-                if (MODE != 1) ring[p] = bload4(rW, lbase + 4 * (s + PF) * H);
+                if (MODE != 1 && MODE < 3) ring[p] = bload4(rW, lbase + 4 * (s + PF) * H);
                 else ring[p].x += 1e-9f;
                 __builtin_amdgcn_sched_barrier(0);
             }
+        }
+        if (MODE == 4) {  // no epilogue, no barriers (timing only)
+            if (l == LAYERS - 1)
+#pragma unroll
+                for (int g = 0; g < CG; ++g) slab[(64 * w + 16 * lk) * NCT + 16 * g + li] = acc[g][0][0] + acc[g][1][1] + acc[g][2][2] + acc[g][3][3];
+            continue;
         }
         __syncthreads();
 #pragma unroll
@@ -205,7 +213,7 @@ __global__ __launch_bounds__(512, 1) void mlp_stream_cg(const float* __restrict_
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     const int f = 64 * w + 16 * lk + 4 * r + c;
-                    slab[f * NCT + 16 * g + li] = gelu_fast(acc[g][c][r] + bb[c]);
+                    slab[f * NCT + 16 * g + li] = MODE == 6 ? acc[g][c][r] + bb[c] : gelu_fast(acc[g][c][r] + bb[c]);
                 }
             }
         __syncthreads();
@@ -434,10 +442,11 @@ int main(int argc, char** argv) {
     std::vector<float> ref(nX);
     CK(hipMemcpy(ref.data(), in, 4 * nX, hipMemcpyDeviceToHost));
     run_cg<8, 1, 0>(nm, iters, W, b, X, Y, ref, ncols, s);
-    run_cg<8, 1, 1>(nm, iters, W, b, X, Y, ref, ncols, s);
-    run_cg<8, 1, 2>(nm, iters, W, b, X, Y, ref, ncols, s);
+
+    run_cg<8, 1, 5>(nm, iters, W, b, X, Y, ref, ncols, s);
+    run_cg<8, 1, 6>(nm, iters, W, b, X, Y, ref, ncols, s);
     run_cg<8, 2, 0>(nm, iters, W, b, X, Y, ref, ncols, s);
-    run_dx<2>(nm, iters, W, b, X, Y, T0, T1, ncols, s);
-    run_dx<4>(nm, iters, W, b, X, Y, T0, T1, ncols, s);
+    run_cg<8, 2, 5>(nm, iters, W, b, X, Y, ref, ncols, s);
+
     return 0;
 }
