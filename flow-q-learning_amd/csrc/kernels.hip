@@ -708,21 +708,26 @@ void launch_gemm_euler_hidden(const GemmArgs& a, hipStream_t s) {
 // (the padded rows multiply finite parameter words by exact zeros).
 constexpr int EF_H = 512, EF_NC = 16, EF_NW = 8, EF_PF = 8, EF_K0MAX = 64;
 
-// tanh(y) = 1 - 2 / (1 + e^{2y}) on v_exp_f32 (no libm branches; saturates
-// to +-1 correctly for |y| large, absolute error ~1e-7 near 0)
-DEV float tanh_fast(float y) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * y)); }
-DEV float gelu_fast(float x) {
-    const float t = tanh_fast(kSqrt2OverPi * (x + 0.044715f * x * x * x));
-    return 0.5f * x * (1.0f + t);
+// GELU-tanh in sigmoid form: 0.5 x (1 + tanh(y)) = x sigmoid(2y), y = k (x +
+// 0.044715 x^3), sigmoid on v_exp_f32 + v_rcp_f32 (no libm branches).  For x
+// very negative exp2 overflows to +inf and rcp gives 0 (gelu -> -0); for x
+// very positive exp2 underflows to 0 (gelu -> x).  5 VALU + 2 transcendental.
+constexpr float kG0 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;  // -2k log2(e)
+constexpr float kG1 = kG0 * 0.044715f;
+DEV float gelu_sig(float x, float x2) {  // sigmoid(2y)
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * fmaf(x2, kG1, kG0)));
 }
+DEV float gelu_fast(float x) { return x * gelu_sig(x, x * x); }
+// d/dx [x s] = s + x s (1 - s) d(2y)/dx,  d(2y)/dx = 2k (1 + 3 * 0.044715 x^2)
+constexpr float kD0 = 2.0f * 0.7978845608028654f, kD1 = kD0 * 3.0f * 0.044715f;
 DEV void gelu_and_grad_fast(float x, float& g, float& gp) {
-    const float t = tanh_fast(kSqrt2OverPi * (x + 0.044715f * x * x * x));
-    g = 0.5f * x * (1.0f + t);
-    gp = 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * kSqrt2OverPi * (1.0f + 3.0f * 0.044715f * x * x);
+    const float x2 = x * x, sg = gelu_sig(x, x2);
+    g = x * sg;
+    gp = fmaf(sg, x * (1.0f - sg) * fmaf(x2, kD1, kD0), sg);
 }
 DEV float gelu_grad_fast(float x) {
-    const float t = tanh_fast(kSqrt2OverPi * (x + 0.044715f * x * x * x));
-    return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * kSqrt2OverPi * (1.0f + 3.0f * 0.044715f * x * x);
+    const float x2 = x * x, sg = gelu_sig(x, x2);
+    return fmaf(sg, x * (1.0f - sg) * fmaf(x2, kD1, kD0), sg);
 }
 
 // One streamed layer's k-loop: acc[c] += W[k][64w + 4li + c] * xs[k][li] over
