@@ -130,6 +130,40 @@ def eval_rollout_leg(pop, wl: dict, n_envs: int, steps: int, dev) -> dict:
                     "termination predictor); host-synchronised wall time incl. H2D of init obs"}
 
 
+def envmodel_train_leg(wl: dict, data: dict, steps: int) -> dict:
+    """Env-model training throughput (outside `value`): the
+    baseline state predictor (128, 256, 128) and the termination predictor, B = 256,
+    device-sampled from the same synthetic buffer, `steps` train_steps each."""
+    import envmodel as em
+    from envmodel.trainer import EnvModelTrainerConfig, StatePredictorTrainer, TerminationPredictorTrainer
+
+    class _Loader:
+        def __init__(self, ds):
+            self.dataset = ds
+
+    spec = em.EnvModelSpec(wl["obs_dim"], wl["action_dim"])
+    ds = {k: data[k] for k in ("observations", "actions", "rewards", "next_observations")}
+    out = {}
+    for name, cls, params, cfg in (
+            ("state_predictor", StatePredictorTrainer, em.init_state_predictor(spec, 0),
+             EnvModelTrainerConfig(steps=steps, termination_weight=0.0)),
+            ("termination_predictor", TerminationPredictorTrainer, em.init_termination_predictor(spec, 1),
+             EnvModelTrainerConfig(steps=steps))):
+        tr = cls(spec, params, _Loader(ds), None, cfg)
+        tr.steps(20)
+        tr.sync()
+        t0 = time.perf_counter()
+        tr.steps(steps)
+        tr.sync()
+        el = time.perf_counter() - t0
+        out[name] = {"train_steps_per_s": round(steps / el, 1), "us_per_step": round(1e6 * el / steps, 2),
+                     "final_train_loss": round(tr.read_logs()["loss"], 6)}
+        tr.close()
+    out["note"] = ("B=256, hidden (128, 256, 128), Adam + cosine decay; two launches per train_step "
+                   "(fused fwd/loss/bwd over 16-row blocks, partial-sum Adam)")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -150,6 +184,8 @@ def main():
     ap.add_argument("--eval-envs", type=int, default=50, help="world-model rollout leg: envs per member "
                     "(reference eval_episodes); 0 disables the leg")
     ap.add_argument("--eval-steps", type=int, default=1000, help="world-model rollout leg: max_episode_steps")
+    ap.add_argument("--envmodel-train-steps", type=int, default=2000,
+                    help="env-model training leg: train_steps per model (0 disables the leg)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -275,6 +311,8 @@ def main():
     }
     if args.eval_envs > 0:
         result["eval_rollout"] = eval_rollout_leg(pop, wl, args.eval_envs, args.eval_steps, dev)
+    if args.envmodel_train_steps > 0 and rank == 0:
+        result["envmodel_train"] = envmodel_train_leg(wl, data, args.envmodel_train_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
         log(f"[rank 0] cpu baseline ({args.cpu_baseline_seconds:.0f} s budget, {threads} threads)")

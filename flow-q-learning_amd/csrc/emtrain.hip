@@ -1,0 +1,774 @@
+// Env-model trainer: one training step of the
+// reference's world-model trainers on the GPU.
+//
+//   state predictor       envmodel/state_predictor_trainer.py:67-95 on
+//                         BaselineStatePredictor (envmodel/baseline.py:25-37),
+//                         state_prediction_loss (envmodel/loss.py:80-111) as bound
+//                         by train_env_model.py:37-44 (reconstruction weight 0;
+//                         a frozen termination predictor scores the predicted next
+//                         observation when termination_weight > 0)
+//   termination predictor envmodel/termination_predictor_trainer.py:55-76 on
+//                         TerminationPredictor (envmodel/termination_predictor.py:
+//                         14-21; input dropout while training), focal_loss
+//                         (envmodel/loss.py:33-66; train_env_model.py:79)
+//   optimiser             optax.adam(cosine_decay_schedule(init_lr, steps))
+//
+// The nets are small (obs 28-42 -> 128 -> 256 -> 128 -> obs), so one step is
+// two launches: em_grad_kernel (block = 16 minibatch rows: forward, loss,
+// backward, per-block partial parameter grads, per-block log sums; activations
+// in LDS, feature-major [feature][row]; the weights stream from L2) and
+// em_adam_kernel (fixed-order sum of the block partials + Adam).  VALU fp32 FMA
+// (each weight load feeds up to 16 rows): the layer widths (33, 28, 1) do not
+// tile onto MFMA shapes and the step is launch-latency bound anyway.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/fqlpop.h"
+#include "kernels.h"
+
+#define DEV __device__ __forceinline__
+
+namespace fq {
+namespace em {
+
+constexpr int R = 16;      // minibatch rows per block
+constexpr int NT = 512;    // threads per block
+constexpr int MAXL = 8;    // Dense layers per net
+constexpr int NLOG = 16;   // per-block log sums
+
+struct Net {
+    int n;                              // Dense layers (hidden + output)
+    int dims[MAXL + 1];                 // dims[0] = input, dims[n] = output
+    long long w[MAXL], b[MAXL];         // flat offsets (flax leaf order)
+    long long ln_scale, ln_bias;        // state predictor LayerNorm_0 (-1: none)
+};
+
+struct StepArgs {
+    int kind;                           // FQLPOP_EM_STATE_PREDICTOR / FQLPOP_EM_TERMINATION
+    int train;                          // 1: grads + dropout; 0: eval logs only
+    Net net, tpn;                       // trained net; frozen termination predictor (kind 0, tw > 0)
+    const float* params;
+    const float* tp;
+    float* part;                        // [blocks][P] partial grads
+    long long P;
+    float* logs;                        // [blocks][NLOG]
+    // rows: injected [B][..] arrays, or gathered from the dataset by Philox indices
+    const float *obs, *act, *rew, *nobs;
+    long long n_rows;
+    int injected;
+    const unsigned char* keep;          // injected dropout keep mask [B][obs] or null
+    uint64_t seed;
+    long long step;                     // update count (sampling counter)
+    int B, D, A;
+    float tw, ttw, alpha, gamma, rate;
+    // LDS carve-up (floats)
+    int lds_floats;
+};
+
+// ----------------------------------------------------------------- Philox
+DEV void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+// uniform [0, 1) from (seed, a, b, c)
+DEV float urand(uint64_t seed, uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t x[4] = {a, b, c, 0x3E7u};
+    philox(x, (uint32_t)seed, (uint32_t)(seed >> 32));
+    return (x[0] >> 8) * (1.0f / 16777216.0f);
+}
+
+DEV float softplus(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
+
+// out[f][r] = act(sum_k W[k][f] in[k][r] + b[f]) for f < N, r < R; thread = (f, row group).
+template <int RPT>
+DEV void dense_fwd_t(const float* __restrict__ W, const float* __restrict__ bias, const float* in, int K, int N,
+                     float* out, bool relu) {
+    constexpr int RG = R / RPT;
+    for (int t = threadIdx.x; t < N * RG; t += NT) {
+        const int f = t % N, r0 = (t / N) * RPT;
+        float acc[RPT];
+        const float bf = bias[f];
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) acc[r] = bf;
+#pragma unroll 4
+        for (int k = 0; k < K; ++k) {
+            const float w = W[(long long)k * N + f];
+            const float* x = in + k * R + r0;
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) acc[r] = fmaf(w, x[r], acc[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) out[f * R + r0 + r] = relu ? fmaxf(acc[r], 0.f) : acc[r];
+    }
+}
+DEV void dense_fwd(const float* W, const float* b, const float* in, int K, int N, float* out, bool relu) {
+    if (N * 16 <= NT) dense_fwd_t<1>(W, b, in, K, N, out, relu);
+    else if (N * 8 <= NT) dense_fwd_t<2>(W, b, in, K, N, out, relu);
+    else if (N * 4 <= NT) dense_fwd_t<4>(W, b, in, K, N, out, relu);
+    else if (N * 2 <= NT) dense_fwd_t<8>(W, b, in, K, N, out, relu);
+    else dense_fwd_t<16>(W, b, in, K, N, out, relu);
+    __syncthreads();
+}
+
+// g_in[k][r] = sum_f W[k][f] g[f][r] (times relu'(in) when mask_in): thread = (k, row group)
+template <int RPT>
+DEV void dense_dx_t(const float* __restrict__ W, const float* g, int K, int N, float* g_in, const float* mask_in) {
+    constexpr int RG = R / RPT;
+    for (int t = threadIdx.x; t < K * RG; t += NT) {
+        const int k = t % K, r0 = (t / K) * RPT;
+        float acc[RPT];
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
+        const float* __restrict__ wr = W + (long long)k * N;
+#pragma unroll 4
+        for (int f = 0; f < N; ++f) {
+            const float w = wr[f];
+            const float* x = g + f * R + r0;
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) acc[r] = fmaf(w, x[r], acc[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            float v = acc[r];
+            if (mask_in && !(mask_in[k * R + r0 + r] > 0.f)) v = 0.f;  // relu' (0 at 0)
+            g_in[k * R + r0 + r] = v;
+        }
+    }
+}
+DEV void dense_dx(const float* W, const float* g, int K, int N, float* g_in, const float* mask_in) {
+    if (K * 16 <= NT) dense_dx_t<1>(W, g, K, N, g_in, mask_in);
+    else if (K * 8 <= NT) dense_dx_t<2>(W, g, K, N, g_in, mask_in);
+    else if (K * 4 <= NT) dense_dx_t<4>(W, g, K, N, g_in, mask_in);
+    else if (K * 2 <= NT) dense_dx_t<8>(W, g, K, N, g_in, mask_in);
+    else dense_dx_t<16>(W, g, K, N, g_in, mask_in);
+    __syncthreads();
+}
+
+// Partial parameter grads of one Dense over the block's rows:
+// dW[k][f] = sum_r in[k][r] g[f][r], db[f] = sum_r g[f][r]
+DEV void dense_dw(const float* in, const float* g, int K, int N, float* __restrict__ pW, float* __restrict__ pb) {
+    for (int t = threadIdx.x; t < K * N; t += NT) {
+        const int k = t / N, f = t % N;
+        const float* a = in + k * R;
+        const float* b = g + f * R;
+        float s = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; ++r) s = fmaf(a[r], b[r], s);
+        pW[t] = s;
+    }
+    for (int f = threadIdx.x; f < N; f += NT) {
+        const float* b = g + f * R;
+        float s = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; ++r) s += b[r];
+        pb[f] = s;
+    }
+}
+
+__global__ __launch_bounds__(NT) void em_grad_kernel(const StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ float lsum[NLOG][R];
+    __shared__ float lab[R];
+    __shared__ long long rowid[R];
+    const int tid = threadIdx.x, blk = blockIdx.x;
+    const Net& N = a.net;
+    const int D = a.D, A = a.A;
+    const int K0 = N.dims[0];
+    // LDS: x0 [K0][R] | xhat [K0][R] | acts[i] [dims[i]][R] i = 0..n (acts[n] = output) |
+    //      gA, gB, gC [maxd][R] | nobs [D][R] | tp acts [dims][R]
+    int maxd = 0;
+    for (int i = 0; i <= N.n; ++i) maxd = max(maxd, N.dims[i]);
+    for (int i = 0; i <= a.tpn.n; ++i) maxd = max(maxd, a.tpn.dims[i]);
+    float* x0 = lds;
+    float* xhat = x0 + K0 * R;
+    float* acts[MAXL + 1];
+    acts[0] = xhat + K0 * R;
+    for (int i = 1; i <= N.n; ++i) acts[i] = acts[i - 1] + N.dims[i - 1] * R;
+    float* gA = acts[N.n] + N.dims[N.n] * R;
+    float* gB = gA + maxd * R;
+    float* gC = gB + maxd * R;
+    float* nobs = gC + maxd * R;
+    float* tacts[MAXL + 1];
+    tacts[0] = nobs + D * R;
+    for (int i = 1; i <= a.tpn.n; ++i) tacts[i] = tacts[i - 1] + a.tpn.dims[i - 1] * R;
+
+    // ---- rows: injected batch rows, or Philox-drawn dataset rows ([EXT] Dataset.sample)
+    if (tid < R) {
+        const int gr = blk * R + tid;
+        long long id = gr;
+        if (!a.injected) {
+            uint32_t c[4] = {(uint32_t)gr, (uint32_t)a.step, 0xE7u, 0u};
+            philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+            id = (long long)((((uint64_t)c[1] << 32) | c[0]) % (uint64_t)a.n_rows);
+        }
+        rowid[tid] = id;
+        lab[tid] = a.rew[id] == 0.f ? 1.f : 0.f;
+    }
+    for (int q = tid; q < NLOG * R; q += NT) lsum[q / R][q % R] = 0.f;
+    __syncthreads();
+    for (int t = tid; t < D * R; t += NT) {
+        const int k = t / R, r = t % R;
+        nobs[t] = a.nobs[rowid[r] * D + k];
+    }
+    if (a.kind == FQLPOP_EM_STATE_PREDICTOR) {
+        for (int t = tid; t < K0 * R; t += NT) {
+            const int k = t / R, r = t % R;
+            x0[t] = k < D ? a.obs[rowid[r] * D + k] : a.act[rowid[r] * A + (k - D)];
+        }
+    } else {
+        // termination predictor: dropout on the input while training; the keep mask is fixed
+        // per (batch position, feature), as the reference's constant dropout rng
+        for (int t = tid; t < K0 * R; t += NT) {
+            const int k = t / R, r = t % R;
+            float v = a.nobs[rowid[r] * D + k];
+            if (a.train) {
+                const int pos = blk * R + r;
+                const bool keep = a.keep ? a.keep[(long long)pos * D + k] != 0
+                                         : urand(a.seed, (uint32_t)pos, (uint32_t)k, 0xD20u) >= a.rate;
+                v = keep ? v / (1.0f - a.rate) : 0.f;
+            }
+            x0[t] = v;
+        }
+    }
+    __syncthreads();
+
+    // ---- forward
+    const float* P = a.params;
+    if (N.ln_scale >= 0) {
+        // flax LayerNorm over the K0 input features of each row (eps 1e-6, E[x^2] - mu^2 clipped)
+        __shared__ float mu_s[R], rs_s[R];
+        if (tid < R) {
+            float s1 = 0.f, s2 = 0.f;
+            for (int k = 0; k < K0; ++k) {
+                const float v = x0[k * R + tid];
+                s1 += v;
+                s2 += v * v;
+            }
+            const float mu = s1 / K0;
+            mu_s[tid] = mu;
+            rs_s[tid] = 1.0f / sqrtf(fmaxf(s2 / K0 - mu * mu, 0.f) + 1e-6f);
+        }
+        __syncthreads();
+        for (int t = tid; t < K0 * R; t += NT) {
+            const int k = t / R, r = t % R;
+            const float xh = (x0[t] - mu_s[r]) * rs_s[r];
+            xhat[t] = xh;
+            acts[0][t] = xh * P[N.ln_scale + k] + P[N.ln_bias + k];
+        }
+    } else {
+        for (int t = tid; t < K0 * R; t += NT) acts[0][t] = x0[t];
+    }
+    __syncthreads();
+    for (int i = 0; i < N.n; ++i)
+        dense_fwd(P + N.w[i], P + N.b[i], acts[i], N.dims[i], N.dims[i + 1], acts[i + 1], i < N.n - 1);
+    const float* out = acts[N.n];
+
+    // ---- loss, output gradient (gA [dout][R]) and log sums
+    const float invB = 1.0f / (float)a.B;
+    if (a.kind == FQLPOP_EM_STATE_PREDICTOR) {
+        // pred = out + obs; MSE(pred, next) over B x D; grads / (1 + tw)
+        const float norm = 1.0f + a.tw;
+        const float gscale = 2.0f / ((float)a.B * D) / norm;
+        float* pred = tacts[0];  // pred [D][R]: the frozen termination predictor's input
+        for (int t = tid; t < D * R; t += NT) {
+            const float p = out[t] + x0[t];  // x0 rows k < D are the observations
+            const float d = p - nobs[t];
+            pred[t] = p;
+            gA[t] = gscale * d;
+            atomicAdd(&lsum[0][t % R], d * d);
+        }
+        __syncthreads();
+        if (a.tw > 0.f) {
+            // frozen termination predictor on pred; weighted BCE (envmodel/loss.py:14-30)
+            const Net& T = a.tpn;
+            for (int i = 0; i < T.n; ++i)
+                dense_fwd(a.tp + T.w[i], a.tp + T.b[i], tacts[i], T.dims[i], T.dims[i + 1], tacts[i + 1],
+                          i < T.n - 1);
+            if (tid < R) {
+                const float x = tacts[T.n][tid], z = lab[tid], w = a.ttw;
+                const float ce = softplus(x) - x * z;
+                lsum[1][tid] = (z > 0.f ? w * ce : ce) / (w + 1.f);
+                lsum[2][tid] = z > 0.f ? ce : 0.f;
+                lsum[3][tid] = z > 0.f ? 0.f : ce;
+                lsum[4][tid] = z;
+                lsum[5][tid] = 1.f - z;
+                const float p = 1.0f / (1.0f + expf(-x));
+                gB[tid] = (z > 0.f ? w : 1.f) / (w + 1.f) * (p - z) * invB;  // d bce / d logit
+            }
+            __syncthreads();
+            // dX down the frozen stack (relu' of each hidden input), gB <-> gC
+            float* src = gB;
+            float* dst = gC;
+            for (int i = T.n - 1; i >= 0; --i) {
+                dense_dx(a.tp + T.w[i], src, T.dims[i], T.dims[i + 1], dst, i > 0 ? tacts[i] : nullptr);
+                float* tmp = src;
+                src = dst;
+                dst = tmp;
+            }
+            for (int t = tid; t < D * R; t += NT) gA[t] += a.tw / norm * src[t];
+            __syncthreads();
+        }
+    } else {
+        // focal loss (alpha, gamma) on the logit
+        if (tid < R) {
+            const float x = out[tid], z = lab[tid];
+            const float p = 1.0f / (1.0f + expf(-x));
+            const float ce = softplus(x) - x * z;
+            const float pt = z > 0.f ? p : 1.f - p;
+            const float af = z > 0.f ? a.alpha : 1.f - a.alpha;
+            const float li = af * powf(1.f - pt, a.gamma) * ce;
+            const float logp = -softplus(-x), log1mp = -softplus(x);
+            const float d = z > 0.f ? powf(1.f - p, a.gamma) * (a.gamma * p * logp - (1.f - p))
+                                    : powf(p, a.gamma) * (-a.gamma * (1.f - p) * log1mp + p);
+            gA[tid] = af * d * invB;
+            lsum[1][tid] = li;
+            lsum[2][tid] = z > 0.f ? li : 0.f;
+            lsum[3][tid] = z > 0.f ? 0.f : li;
+            lsum[4][tid] = z;
+            lsum[5][tid] = 1.f - z;
+            const bool pr = x > 0.f;
+            lsum[6][tid] = (pr == (z > 0.f)) ? 1.f : 0.f;
+            lsum[7][tid] = (pr && z > 0.f) ? 1.f : 0.f;
+            lsum[8][tid] = pr ? 1.f : 0.f;
+        }
+        __syncthreads();
+    }
+
+    // ---- block log sums
+    if (tid < NLOG) {
+        float s = 0.f;
+        for (int r = 0; r < R; ++r) s += lsum[tid][r];
+        a.logs[(long long)blk * NLOG + tid] = s;
+    }
+    if (!a.train) return;
+
+    // ---- backward: partial grads of every Dense (and LayerNorm_0)
+    float* pg = a.part + (long long)blk * a.P;
+    float* g = gA;
+    float* gn = gB;
+    for (int i = N.n - 1; i >= 0; --i) {
+        dense_dw(acts[i], g, N.dims[i], N.dims[i + 1], pg + N.w[i], pg + N.b[i]);
+        if (i > 0 || N.ln_scale >= 0) dense_dx(P + N.w[i], g, N.dims[i], N.dims[i + 1], gn, i > 0 ? acts[i] : nullptr);
+        else __syncthreads();
+        float* tmp = g;
+        g = gn;
+        gn = tmp;
+    }
+    if (N.ln_scale >= 0) {
+        // g = grad wrt the LayerNorm output [K0][R]
+        for (int k = tid; k < K0; k += NT) {
+            float ss = 0.f, sb = 0.f;
+            for (int r = 0; r < R; ++r) {
+                ss += g[k * R + r] * xhat[k * R + r];
+                sb += g[k * R + r];
+            }
+            pg[N.ln_scale + k] = ss;
+            pg[N.ln_bias + k] = sb;
+        }
+    }
+}
+
+struct AdamArgsEm {
+    float* params;
+    float *m, *v;
+    const float* part;
+    long long P;
+    int blocks;
+    float lr, bc1, bc2;
+};
+
+// Fixed-order sum of the block partials + optax.adam
+__global__ __launch_bounds__(256) void em_adam_kernel(const AdamArgsEm a) {
+    const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (p >= a.P) return;
+    float g = 0.f;
+    for (int b = 0; b < a.blocks; ++b) g += a.part[(long long)b * a.P + p];
+    const float m = 0.1f * g + 0.9f * a.m[p];
+    const float v = 0.001f * (g * g) + 0.999f * a.v[p];
+    a.m[p] = m;
+    a.v[p] = v;
+    a.params[p] = a.params[p] + (-a.lr) * ((m / a.bc1) / (sqrtf(v / a.bc2) + 1e-8f));
+}
+
+}  // namespace em
+}  // namespace fq
+
+// ===================================================================== ABI ==
+using namespace fq::em;
+
+namespace {
+thread_local std::string em_err;
+struct EmErr {
+    int code;
+    std::string msg;
+};
+#define EMCHK(x)                                                                          \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) throw EmErr{FQLPOP_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+    } while (0)
+#define EMARG(c, m)                                          \
+    do {                                                     \
+        if (!(c)) throw EmErr{FQLPOP_E_ARG, std::string(m)}; \
+    } while (0)
+template <class F>
+int em_guard(F&& f) {
+    try {
+        f();
+        em_err.clear();
+        return FQLPOP_OK;
+    } catch (const EmErr& e) {
+        em_err = e.msg;
+        fq::set_last_error(e.msg.c_str());
+        return e.code;
+    }
+}
+
+// flax leaf order (path-sorted): Dense_i/bias, Dense_i/kernel ..., LayerNorm_0/bias, LayerNorm_0/scale
+Net layout(int in, int nh, const int* hid, int out, bool ln, long long* total) {
+    Net n{};
+    n.n = nh + 1;
+    EMARG(n.n <= MAXL, "too many layers");
+    n.dims[0] = in;
+    for (int i = 0; i < nh; ++i) n.dims[i + 1] = hid[i];
+    n.dims[nh + 1] = out;
+    long long o = 0;
+    for (int i = 0; i < n.n; ++i) {
+        n.b[i] = o;
+        o += n.dims[i + 1];
+        n.w[i] = o;
+        o += (long long)n.dims[i] * n.dims[i + 1];
+    }
+    n.ln_scale = n.ln_bias = -1;
+    if (ln) {
+        n.ln_bias = o;
+        o += in;
+        n.ln_scale = o;
+        o += in;
+    }
+    *total = o;
+    return n;
+}
+}  // namespace
+
+struct fqlpop_emtrain {
+    fqlpop_emtrain_config cfg{};
+    int device = 0;
+    Net net{}, tpn{};
+    long long P = 0, PT = 0;
+    float *params = nullptr, *m = nullptr, *v = nullptr, *part = nullptr, *logs = nullptr, *tp = nullptr;
+    float *d_obs = nullptr, *d_act = nullptr, *d_rew = nullptr, *d_nobs = nullptr;
+    long long n_rows = 0;
+    float *i_obs = nullptr, *i_act = nullptr, *i_rew = nullptr, *i_nobs = nullptr;
+    unsigned char* i_keep = nullptr;
+    long long count = 0;
+    int blocks = 0;
+    int lds_bytes = 0;
+    hipStream_t s = nullptr;
+};
+
+static void em_free(fqlpop_emtrain* h) {
+    for (void* p : {(void*)h->params, (void*)h->m, (void*)h->v, (void*)h->part, (void*)h->logs, (void*)h->tp,
+                    (void*)h->d_obs, (void*)h->d_act, (void*)h->d_rew, (void*)h->d_nobs, (void*)h->i_obs,
+                    (void*)h->i_act, (void*)h->i_rew, (void*)h->i_nobs, (void*)h->i_keep})
+        if (p) (void)hipFree(p);
+    if (h->s) (void)hipStreamDestroy(h->s);
+}
+
+static void em_layouts(const fqlpop_emtrain_config* c, Net* net, long long* P, Net* tpn, long long* PT) {
+    EMARG(c->obs_dim > 0 && c->action_dim >= 0, "bad obs/action dims");
+    EMARG(c->num_hidden >= 0 && c->num_hidden < MAXL, "bad num_hidden");
+    for (int i = 0; i < c->num_hidden; ++i) EMARG(c->hidden_dims[i] > 0 && c->hidden_dims[i] <= 1024, "bad hidden dim");
+    if (c->kind == FQLPOP_EM_STATE_PREDICTOR) {
+        *net = layout(c->obs_dim + c->action_dim, c->num_hidden, c->hidden_dims, c->obs_dim, true, P);
+        *PT = 0;
+        if (c->termination_weight > 0.f) {
+            EMARG(c->tp_num_hidden >= 0 && c->tp_num_hidden < MAXL, "bad tp_num_hidden");
+            *tpn = layout(c->obs_dim, c->tp_num_hidden, c->tp_hidden_dims, 1, false, PT);
+        } else {
+            *tpn = Net{};
+            tpn->ln_scale = tpn->ln_bias = -1;
+        }
+    } else {
+        EMARG(c->kind == FQLPOP_EM_TERMINATION, "kind must be FQLPOP_EM_STATE_PREDICTOR or FQLPOP_EM_TERMINATION");
+        *net = layout(c->obs_dim, c->num_hidden, c->hidden_dims, 1, false, P);
+        *tpn = Net{};
+        tpn->ln_scale = tpn->ln_bias = -1;
+        *PT = 0;
+    }
+}
+
+extern "C" {
+
+int fqlpop_emtrain_param_count(const fqlpop_emtrain_config* cfg, int64_t* n_params) {
+    return em_guard([&] {
+        EMARG(cfg && n_params, "null argument");
+        Net a, b;
+        long long P, PT;
+        em_layouts(cfg, &a, &P, &b, &PT);
+        *n_params = P;
+    });
+}
+
+int fqlpop_emtrain_create(const fqlpop_emtrain_config* cfg, const float* params, int64_t n_params, int device,
+                          fqlpop_emtrain_t** out) {
+    return em_guard([&] {
+        EMARG(cfg && params && out, "null argument");
+        EMARG(cfg->batch_size > 0 && cfg->batch_size % R == 0, "batch_size must be a positive multiple of 16");
+        EMARG(cfg->steps > 0, "steps must be > 0");
+        auto h = std::make_unique<fqlpop_emtrain>();
+        h->cfg = *cfg;
+        h->device = device;
+        em_layouts(cfg, &h->net, &h->P, &h->tpn, &h->PT);
+        EMARG(n_params == h->P, "params size mismatch");
+        EMCHK(hipSetDevice(device));
+        // LDS: x0, xhat [K0][R], acts [sum dims][R], gA, gB [maxd][R], nobs [D][R], tp acts
+        int maxd = 0, sum = 0, tsum = 0;
+        for (int i = 0; i <= h->net.n; ++i) { maxd = std::max(maxd, h->net.dims[i]); sum += h->net.dims[i]; }
+        for (int i = 0; i <= h->tpn.n && h->tpn.n > 0; ++i) { maxd = std::max(maxd, h->tpn.dims[i]); tsum += h->tpn.dims[i]; }
+        const long long fl = (long long)R * (2 * h->net.dims[0] + sum + 3 * maxd + cfg->obs_dim + tsum);
+        EMARG(fl * 4 <= 150 * 1024, "env-model layer widths exceed the LDS budget of the fused step");
+        h->lds_bytes = (int)(fl * 4);
+        h->blocks = cfg->batch_size / R;
+        const long long P = h->P;
+        EMCHK(hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking));
+        EMCHK(hipMalloc(&h->params, 4 * P));
+        EMCHK(hipMalloc(&h->m, 4 * P));
+        EMCHK(hipMalloc(&h->v, 4 * P));
+        EMCHK(hipMalloc(&h->part, 4 * P * h->blocks));
+        EMCHK(hipMalloc(&h->logs, 4 * (long long)NLOG * h->blocks));
+        EMCHK(hipMemcpy(h->params, params, 4 * P, hipMemcpyHostToDevice));
+        EMCHK(hipMemset(h->m, 0, 4 * P));
+        EMCHK(hipMemset(h->v, 0, 4 * P));
+        EMCHK(hipMemset(h->logs, 0, 4 * (long long)NLOG * h->blocks));
+        const long long B = cfg->batch_size, D = cfg->obs_dim, A = cfg->action_dim;
+        EMCHK(hipMalloc(&h->i_obs, 4 * B * D));
+        EMCHK(hipMalloc(&h->i_act, 4 * std::max(1LL, B * A)));
+        EMCHK(hipMalloc(&h->i_rew, 4 * B));
+        EMCHK(hipMalloc(&h->i_nobs, 4 * B * D));
+        EMCHK(hipMalloc(&h->i_keep, B * D));
+        EMCHK(hipFuncSetAttribute((const void*)em_grad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
+        *out = h.release();
+    });
+}
+
+int fqlpop_emtrain_destroy(fqlpop_emtrain_t* h) {
+    return em_guard([&] {
+        if (!h) return;
+        (void)hipSetDevice(h->device);
+        (void)hipDeviceSynchronize();
+        em_free(h);
+        delete h;
+    });
+}
+
+int fqlpop_emtrain_set_frozen_termination(fqlpop_emtrain_t* h, const float* tp_params, int64_t n) {
+    return em_guard([&] {
+        EMARG(h && tp_params, "null argument");
+        EMARG(h->PT > 0, "no frozen termination predictor in this config (termination_weight == 0)");
+        EMARG(n == h->PT, "termination predictor size mismatch");
+        EMCHK(hipSetDevice(h->device));
+        if (!h->tp) EMCHK(hipMalloc(&h->tp, 4 * h->PT));
+        EMCHK(hipMemcpy(h->tp, tp_params, 4 * h->PT, hipMemcpyHostToDevice));
+    });
+}
+
+int fqlpop_emtrain_set_dataset(fqlpop_emtrain_t* h, const float* obs, const float* act, const float* rew,
+                               const float* next_obs, int64_t n_rows) {
+    return em_guard([&] {
+        EMARG(h && obs && rew && next_obs && (act || h->cfg.action_dim == 0), "null argument");
+        EMARG(n_rows > 0, "n_rows must be > 0");
+        EMCHK(hipSetDevice(h->device));
+        for (float* p : {h->d_obs, h->d_act, h->d_rew, h->d_nobs})
+            if (p) EMCHK(hipFree(p));
+        const long long D = h->cfg.obs_dim, A = h->cfg.action_dim;
+        EMCHK(hipMalloc(&h->d_obs, 4 * n_rows * D));
+        EMCHK(hipMalloc(&h->d_act, 4 * std::max(1LL, n_rows * A)));
+        EMCHK(hipMalloc(&h->d_rew, 4 * n_rows));
+        EMCHK(hipMalloc(&h->d_nobs, 4 * n_rows * D));
+        EMCHK(hipMemcpy(h->d_obs, obs, 4 * n_rows * D, hipMemcpyHostToDevice));
+        if (A) EMCHK(hipMemcpy(h->d_act, act, 4 * n_rows * A, hipMemcpyHostToDevice));
+        EMCHK(hipMemcpy(h->d_rew, rew, 4 * n_rows, hipMemcpyHostToDevice));
+        EMCHK(hipMemcpy(h->d_nobs, next_obs, 4 * n_rows * D, hipMemcpyHostToDevice));
+        h->n_rows = n_rows;
+    });
+}
+
+static StepArgs em_args(fqlpop_emtrain* h, bool train, bool injected) {
+    const auto& c = h->cfg;
+    StepArgs a{};
+    a.kind = c.kind;
+    a.train = train ? 1 : 0;
+    a.net = h->net;
+    a.tpn = h->tpn;
+    a.params = h->params;
+    a.tp = h->tp;
+    a.part = h->part;
+    a.P = h->P;
+    a.logs = h->logs;
+    a.injected = injected ? 1 : 0;
+    if (injected) {
+        a.obs = h->i_obs; a.act = h->i_act; a.rew = h->i_rew; a.nobs = h->i_nobs;
+        a.n_rows = c.batch_size;
+    } else {
+        a.obs = h->d_obs; a.act = h->d_act; a.rew = h->d_rew; a.nobs = h->d_nobs;
+        a.n_rows = h->n_rows;
+    }
+    a.seed = c.seed;
+    a.step = h->count;
+    a.B = c.batch_size; a.D = c.obs_dim; a.A = c.action_dim;
+    a.tw = c.kind == FQLPOP_EM_STATE_PREDICTOR ? c.termination_weight : 0.f;
+    a.ttw = c.true_termination_weight;
+    a.alpha = c.focal_alpha; a.gamma = c.focal_gamma; a.rate = c.dropout_rate;
+    return a;
+}
+
+static void em_launch_step(fqlpop_emtrain* h, const StepArgs& a) {
+    hipLaunchKernelGGL(em_grad_kernel, dim3(h->blocks), dim3(NT), h->lds_bytes, h->s, a);
+    EMCHK(hipGetLastError());
+    if (!a.train) return;
+    // optax.cosine_decay_schedule(init, steps)(count), adam bias correction with count + 1
+    const auto& c = h->cfg;
+    const double cc = (double)std::min<long long>(h->count, c.steps);
+    AdamArgsEm ad{};
+    ad.params = h->params; ad.m = h->m; ad.v = h->v; ad.part = h->part;
+    ad.P = h->P; ad.blocks = h->blocks;
+    ad.lr = (float)(c.init_lr * 0.5 * (1.0 + std::cos(3.14159265358979323846 * cc / c.steps)));
+    ad.bc1 = (float)(1.0 - std::pow(0.9, (double)(h->count + 1)));
+    ad.bc2 = (float)(1.0 - std::pow(0.999, (double)(h->count + 1)));
+    hipLaunchKernelGGL(em_adam_kernel, dim3((unsigned)((h->P + 255) / 256)), dim3(256), 0, h->s, ad);
+    EMCHK(hipGetLastError());
+    ++h->count;
+}
+
+static void em_check_ready(fqlpop_emtrain* h) {
+    if (h->cfg.kind == FQLPOP_EM_STATE_PREDICTOR && h->cfg.termination_weight > 0.f && !h->tp)
+        throw EmErr{FQLPOP_E_STATE, "termination_weight > 0 needs fqlpop_emtrain_set_frozen_termination"};
+}
+
+int fqlpop_emtrain_step(fqlpop_emtrain_t* h, int n_steps) {
+    return em_guard([&] {
+        EMARG(h && n_steps >= 0, "bad argument");
+        EMARG(h->n_rows > 0, "no dataset: call fqlpop_emtrain_set_dataset");
+        em_check_ready(h);
+        EMCHK(hipSetDevice(h->device));
+        for (int i = 0; i < n_steps; ++i) em_launch_step(h, em_args(h, true, false));
+    });
+}
+
+static void em_upload_batch(fqlpop_emtrain* h, const float* obs, const float* act, const float* rew,
+                            const float* next_obs) {
+    EMARG(obs && rew && next_obs && (act || h->cfg.action_dim == 0), "null batch array");
+    const long long B = h->cfg.batch_size, D = h->cfg.obs_dim, A = h->cfg.action_dim;
+    EMCHK(hipMemcpyAsync(h->i_obs, obs, 4 * B * D, hipMemcpyHostToDevice, h->s));
+    if (A) EMCHK(hipMemcpyAsync(h->i_act, act, 4 * B * A, hipMemcpyHostToDevice, h->s));
+    EMCHK(hipMemcpyAsync(h->i_rew, rew, 4 * B, hipMemcpyHostToDevice, h->s));
+    EMCHK(hipMemcpyAsync(h->i_nobs, next_obs, 4 * B * D, hipMemcpyHostToDevice, h->s));
+}
+
+int fqlpop_emtrain_step_injected(fqlpop_emtrain_t* h, const float* obs, const float* act, const float* rew,
+                                 const float* next_obs, const uint8_t* keep_mask) {
+    return em_guard([&] {
+        EMARG(h, "null handle");
+        em_check_ready(h);
+        EMCHK(hipSetDevice(h->device));
+        em_upload_batch(h, obs, act, rew, next_obs);
+        StepArgs a = em_args(h, true, true);
+        if (keep_mask) {
+            EMCHK(hipMemcpyAsync(h->i_keep, keep_mask, (size_t)h->cfg.batch_size * h->cfg.obs_dim,
+                                 hipMemcpyHostToDevice, h->s));
+            a.keep = h->i_keep;
+        }
+        em_launch_step(h, a);
+        EMCHK(hipStreamSynchronize(h->s));  // host batch buffers are reused
+    });
+}
+
+// logs [FQLPOP_EM_LOG_STRIDE] from the per-block sums (layout: include/fqlpop.h)
+static void em_logs(fqlpop_emtrain* h, float* out) {
+    std::vector<float> lg((size_t)NLOG * h->blocks);
+    EMCHK(hipMemcpyAsync(lg.data(), h->logs, 4 * lg.size(), hipMemcpyDeviceToHost, h->s));
+    EMCHK(hipStreamSynchronize(h->s));
+    double s[NLOG] = {0};
+    for (int b = 0; b < h->blocks; ++b)
+        for (int k = 0; k < NLOG; ++k) s[k] += lg[(size_t)b * NLOG + k];
+    const double B = h->cfg.batch_size, D = h->cfg.obs_dim;
+    for (int k = 0; k < FQLPOP_EM_LOG_STRIDE; ++k) out[k] = 0.f;
+    if (h->cfg.kind == FQLPOP_EM_STATE_PREDICTOR) {
+        const double mse = s[0] / (B * D), tw = h->cfg.termination_weight;
+        const double tl = tw > 0 ? s[1] / B : 0.0;
+        out[0] = (float)((mse + tw * tl) / (1.0 + tw));
+        out[1] = (float)mse;
+        out[2] = (float)tl;
+        out[3] = (float)(s[4] > 0 ? s[2] / s[4] : NAN);
+        out[4] = (float)(s[5] > 0 ? s[3] / s[5] : NAN);
+    } else {
+        out[0] = (float)(s[1] / B);
+        out[1] = (float)(s[2] / (s[4] + 1e-8));
+        out[2] = (float)(s[3] / (s[5] + 1e-8));
+        out[3] = (float)(s[6] / B);
+        out[4] = (float)(s[8] > 0 ? s[7] / s[8] : 1.0);
+        out[5] = (float)(s[4] > 0 ? s[7] / s[4] : 1.0);
+    }
+}
+
+int fqlpop_emtrain_read_logs(fqlpop_emtrain_t* h, float* logs) {
+    return em_guard([&] {
+        EMARG(h && logs, "null argument");
+        EMCHK(hipSetDevice(h->device));
+        em_logs(h, logs);
+    });
+}
+
+int fqlpop_emtrain_eval(fqlpop_emtrain_t* h, const float* obs, const float* act, const float* rew,
+                        const float* next_obs, float* logs) {
+    return em_guard([&] {
+        EMARG(h && logs, "null argument");
+        em_check_ready(h);
+        EMCHK(hipSetDevice(h->device));
+        em_upload_batch(h, obs, act, rew, next_obs);
+        em_launch_step(h, em_args(h, false, true));
+        em_logs(h, logs);
+    });
+}
+
+int fqlpop_emtrain_get_params(fqlpop_emtrain_t* h, int which, float* out, int64_t n) {
+    return em_guard([&] {
+        EMARG(h && out, "null argument");
+        EMARG(n == h->P, "params size mismatch");
+        EMARG(which >= 0 && which <= 2, "which must be FQLPOP_STATE_PARAMS/ADAM_M/ADAM_V");
+        EMCHK(hipSetDevice(h->device));
+        const float* src = which == 0 ? h->params : which == 1 ? h->m : h->v;
+        EMCHK(hipMemcpyAsync(out, src, 4 * n, hipMemcpyDeviceToHost, h->s));
+        EMCHK(hipStreamSynchronize(h->s));
+    });
+}
+
+int fqlpop_emtrain_get_count(fqlpop_emtrain_t* h, int64_t* count) {
+    return em_guard([&] {
+        EMARG(h && count, "null argument");
+        *count = h->count;
+    });
+}
+
+int fqlpop_emtrain_sync(fqlpop_emtrain_t* h) {
+    return em_guard([&] {
+        EMARG(h, "null handle");
+        EMCHK(hipSetDevice(h->device));
+        EMCHK(hipStreamSynchronize(h->s));
+    });
+}
+
+}  // extern "C"

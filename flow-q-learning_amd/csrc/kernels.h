@@ -69,6 +69,7 @@ struct AdamEpi {
     int n_total_chunks;
     const int* count;
     float lr, tau;
+    int mode;                         // 0; timing probes (FQLPOP_DW_MODE): 1 = no optimiser pass, 2 = one k-slice
 };
 struct GemmGroupArgs {
     GemmArgs g[GEMM_GROUP_MAX];
@@ -374,5 +375,9 @@ struct RolloutArgs {
 };
 bool rollout_supported(int H, int L, int D, int A);
 void launch_rollout(const RolloutArgs& a, hipStream_t s);
+
+// The C ABI's thread-local last-error message (runtime.cpp), for entry points
+// defined in other translation units (emtrain.hip).
+void set_last_error(const char* msg);
 
 }  // namespace fq

@@ -192,7 +192,7 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
     const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
     const float lr = e.lr, tau = e.tau;
     float mx = -INFINITY, mn = INFINITY, ss = 0.f;
-    const int rows = min(BM, gM - i0);
+    const int rows = e.mode == 1 ? 0 : min(BM, gM - i0);  // mode 1: timing probe only (no optimiser traffic)
     // pass 1: thread -> 4 consecutive columns of a row; U iterations in flight
     constexpr int TPR = BN / 4, RPI = 256 / TPR, U = 4;  // threads per row, rows per iteration
     const int cj = (tid % TPR) * 4, ri = tid / TPR;
@@ -250,7 +250,7 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
         st[2] = ss;
     }
     // pass 2 (hidden layers: M = H, full tiles): W^T[j][i0 .. i0+BM) as float4 runs along i
-    if (e.wt_off[gi] >= 0) {
+    if (e.wt_off[gi] >= 0 && e.mode != 1) {
         float* __restrict__ WT = e.wt_out + (long long)slot * e.PTT + e.wt_off[gi] + (long long)y * e.wt_sy;
         constexpr int TPC = BM / 4;  // threads per W^T row segment
 #pragma unroll 4
@@ -315,7 +315,7 @@ DEV void gemm_body(const GemmArgs& g, int w, float* smem, const AdamEpi* ae = nu
             }
 
     float4 ra[A_LD], rb[B_LD];
-    const int nk = (gK + BK - 1) / BK;
+    const int nk = (EPI == EPI_ADAM && ae->mode == 2) ? 1 : (gK + BK - 1) / BK;  // mode 2: timing probe only
 #pragma unroll
     for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, ARC>(rA, lda, p, i0, 0);
 #pragma unroll

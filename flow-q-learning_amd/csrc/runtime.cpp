@@ -664,6 +664,10 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         ae.stats = h->stats; ae.n_total_chunks = h->n_chunks_total;
         ae.count = h->count;
         ae.lr = h->cfg.lr; ae.tau = h->cfg.tau;
+        {
+            const char* dm = std::getenv("FQLPOP_DW_MODE");
+            ae.mode = dm ? std::atoi(dm) : 0;
+        }
         launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw, &ae);
     } else if (N.L <= GEMM_GROUP_MAX && N.H % 128 == 0) {
         launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw);
@@ -1176,6 +1180,8 @@ void check_member(fqlpop* h, int member) {
 }
 
 }  // namespace
+
+void fq::set_last_error(const char* msg) { g_err = msg ? msg : ""; }
 
 // =================================================================== C ABI ==
 extern "C" {

@@ -57,8 +57,25 @@ class EnvModelConfig(ctypes.Structure):
     ]
 
 
+class EmTrainConfig(ctypes.Structure):
+    """Mirror of ``fqlpop_emtrain_config`` (include/fqlpop.h)."""
+    _fields_ = [
+        ("kind", ctypes.c_int), ("obs_dim", ctypes.c_int), ("action_dim", ctypes.c_int),
+        ("num_hidden", ctypes.c_int), ("hidden_dims", ctypes.c_int * 8),
+        ("batch_size", ctypes.c_int), ("steps", ctypes.c_int),
+        ("init_lr", ctypes.c_float), ("termination_weight", ctypes.c_float),
+        ("true_termination_weight", ctypes.c_float), ("focal_alpha", ctypes.c_float),
+        ("focal_gamma", ctypes.c_float), ("dropout_rate", ctypes.c_float),
+        ("seed", ctypes.c_uint64),
+        ("tp_num_hidden", ctypes.c_int), ("tp_hidden_dims", ctypes.c_int * 8),
+    ]
+
+
+EM_STATE_PREDICTOR, EM_TERMINATION = 0, 1
+EM_LOG_STRIDE = 8
 _P = ctypes.c_void_p
 _F = ctypes.POINTER(ctypes.c_float)
+_U8 = ctypes.POINTER(ctypes.c_uint8)
 _SIGS = {
     "fqlpop_last_error": (ctypes.c_char_p, []),
     "fqlpop_create": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.c_int, _F,
@@ -103,6 +120,19 @@ _SIGS = {
                                             ctypes.c_int64]),
     "fqlpop_rollout": (ctypes.c_int, [_P, _F, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, _F, _F, _F]),
     "fqlpop_envmodel_step": (ctypes.c_int, [_P, _F, _F, ctypes.c_int, _F, _F]),
+    "fqlpop_emtrain_param_count": (ctypes.c_int, [ctypes.POINTER(EmTrainConfig), ctypes.POINTER(ctypes.c_int64)]),
+    "fqlpop_emtrain_create": (ctypes.c_int, [ctypes.POINTER(EmTrainConfig), _F, ctypes.c_int64, ctypes.c_int,
+                                             ctypes.POINTER(_P)]),
+    "fqlpop_emtrain_destroy": (ctypes.c_int, [_P]),
+    "fqlpop_emtrain_set_frozen_termination": (ctypes.c_int, [_P, _F, ctypes.c_int64]),
+    "fqlpop_emtrain_set_dataset": (ctypes.c_int, [_P, _F, _F, _F, _F, ctypes.c_int64]),
+    "fqlpop_emtrain_step": (ctypes.c_int, [_P, ctypes.c_int]),
+    "fqlpop_emtrain_step_injected": (ctypes.c_int, [_P, _F, _F, _F, _F, _U8]),
+    "fqlpop_emtrain_eval": (ctypes.c_int, [_P, _F, _F, _F, _F, _F]),
+    "fqlpop_emtrain_read_logs": (ctypes.c_int, [_P, _F]),
+    "fqlpop_emtrain_get_params": (ctypes.c_int, [_P, ctypes.c_int, _F, ctypes.c_int64]),
+    "fqlpop_emtrain_get_count": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64)]),
+    "fqlpop_emtrain_sync": (ctypes.c_int, [_P]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
 

@@ -221,6 +221,76 @@ int fqlpop_rollout(fqlpop_t* h, const float* init_obs, int n_envs, int max_steps
  * (terminated = logit > 0).  Host arrays; synchronises. */
 int fqlpop_envmodel_step(fqlpop_t* h, const float* obs, const float* actions, int n, float* next_obs, float* logits);
 
+/* ---------------------------------------------------------------------------
+ * Env-model trainer: the reference's world-model
+ * trainers, one fused GPU step per train_step.
+ *   FQLPOP_EM_STATE_PREDICTOR: StatePredictorTrainer.train_step
+ *     (envmodel/state_predictor_trainer.py:67-95) on BaselineStatePredictor
+ *     (envmodel/baseline.py:25-37) with state_prediction_loss
+ *     (envmodel/loss.py:80-111, reconstruction_weight 0 as train_env_model.py:37-44
+ *     binds it; termination_weight > 0 scores the predicted next observation with
+ *     a frozen termination predictor, fqlpop_emtrain_set_frozen_termination).
+ *   FQLPOP_EM_TERMINATION: TerminationPredictorTrainer.train_step
+ *     (envmodel/termination_predictor_trainer.py:55-76) on TerminationPredictor
+ *     (envmodel/termination_predictor.py:14-21, input dropout) with focal_loss
+ *     (envmodel/loss.py:33-66, train_env_model.py:79).
+ *   Optimiser: optax.adam(optax.cosine_decay_schedule(init_lr, steps))
+ *     (state_predictor_trainer.py:57-61).
+ * Parameters are flat vectors in flax leaf order (path-sorted): Dense_i/bias,
+ * Dense_i/kernel ([in][out]) ..., then LayerNorm_0/bias, LayerNorm_0/scale. */
+enum { FQLPOP_EM_STATE_PREDICTOR = 0, FQLPOP_EM_TERMINATION = 1 };
+#define FQLPOP_EM_LOG_STRIDE 8
+/* logs: state predictor  [loss, next_observation_loss, termination_loss,
+ *                         true_termination_loss, false_termination_loss]
+ *       termination      [loss, true_loss, false_loss, accuracy, precision, recall]
+ *       (accuracy / precision / recall: eval only; envmodel/termination_predictor_trainer.py:78-112) */
+typedef struct fqlpop_emtrain_config {
+    int kind;                      /* FQLPOP_EM_* */
+    int obs_dim, action_dim;
+    int num_hidden;
+    int hidden_dims[8];            /* --model.hidden_dims, default (128, 256, 128) (argparser.py:184-189) */
+    int batch_size;                /* multiple of 16 (256) */
+    int steps;                     /* cosine decay horizon (TrainerConfig.steps) */
+    float init_lr;                 /* 1e-3 */
+    float termination_weight;      /* state predictor (argparser default 1.0; baseline scripts 0) */
+    float true_termination_weight; /* 30 */
+    float focal_alpha, focal_gamma;/* 0.25, 2 */
+    float dropout_rate;            /* 0.1 */
+    uint64_t seed;                 /* device sampling and the fixed dropout mask */
+    int tp_num_hidden;             /* frozen termination predictor (termination_weight > 0) */
+    int tp_hidden_dims[8];
+} fqlpop_emtrain_config;
+typedef struct fqlpop_emtrain fqlpop_emtrain_t;
+
+int fqlpop_emtrain_param_count(const fqlpop_emtrain_config* cfg, int64_t* n_params);
+/* Replaces TrainState.create(params=model.init(...), tx=adam(schedule)) of the
+ * trainers' __init__; params are the initial flat parameters (host, copied). */
+int fqlpop_emtrain_create(const fqlpop_emtrain_config* cfg, const float* params, int64_t n_params, int device,
+                          fqlpop_emtrain_t** out);
+int fqlpop_emtrain_destroy(fqlpop_emtrain_t* h);
+/* utils/envmodel.py load_model("termination_predictor") of the state trainer's __init__. */
+int fqlpop_emtrain_set_frozen_termination(fqlpop_emtrain_t* h, const float* tp_params, int64_t n);
+/* The StepLoader's dataset (utils/data_loader.py:47-52), uploaded once: rows sampled on
+ * device (uniform with replacement, Philox keyed by seed and step). */
+int fqlpop_emtrain_set_dataset(fqlpop_emtrain_t* h, const float* obs, const float* act, const float* rew,
+                               const float* next_obs, int64_t n_rows);
+/* n_steps train_steps on device-sampled batches (asynchronous). */
+int fqlpop_emtrain_step(fqlpop_emtrain_t* h, int n_steps);
+/* One train_step on a host batch [batch_size][..]; keep_mask: NULL (the handle's fixed
+ * Philox dropout mask) or [batch_size][obs_dim] bytes (termination kind). Synchronises. */
+int fqlpop_emtrain_step_injected(fqlpop_emtrain_t* h, const float* obs, const float* act, const float* rew,
+                                 const float* next_obs, const uint8_t* keep_mask);
+/* eval_step on a host batch (no dropout, no update): logs[FQLPOP_EM_LOG_STRIDE]. */
+int fqlpop_emtrain_eval(fqlpop_emtrain_t* h, const float* obs, const float* act, const float* rew,
+                        const float* next_obs, float* logs);
+/* Logs of the last train step; synchronises. */
+int fqlpop_emtrain_read_logs(fqlpop_emtrain_t* h, float* logs);
+/* which = FQLPOP_STATE_PARAMS / _ADAM_M / _ADAM_V; flax.serialization.to_bytes source
+ * (train_env_model.py:132-134). Synchronises. */
+int fqlpop_emtrain_get_params(fqlpop_emtrain_t* h, int which, float* out, int64_t n);
+int fqlpop_emtrain_get_count(fqlpop_emtrain_t* h, int64_t* count);
+int fqlpop_emtrain_sync(fqlpop_emtrain_t* h);
+
 /* Algorithmic GEMM FLOPs of one member-update at the handle's config
  * (SURVEY.md 8d formula). */
 double fqlpop_flops_per_member_step(const fqlpop_config* cfg);

@@ -1,0 +1,187 @@
+"""GPU parity of the env-model trainer (fqlpop_emtrain_*)
+against the float64 restatement in oracle/envmodel_train_oracle.py: injected
+batches, logs and parameters after every step; device sampling: determinism
+and a loss that falls on a learnable synthetic dynamics."""
+import numpy as np
+import pytest
+
+import envmodel as em
+from envmodel.trainer import EnvModelTrainerConfig, StatePredictorTrainer, TerminationPredictorTrainer
+from oracle import envmodel_train_oracle as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(rng, B, D, A, p_term=0.25):
+    obs = rng.standard_normal((B, D)).astype(np.float32)
+    return {"observations": obs, "actions": rng.uniform(-1, 1, (B, A)).astype(np.float32),
+            "next_observations": (obs + 0.1 * rng.standard_normal((B, D))).astype(np.float32),
+            "rewards": np.where(rng.uniform(size=B) < p_term, 0.0, -1.0).astype(np.float32)}
+
+
+def _f64(tree):
+    return {m: {k: np.asarray(v, np.float64) for k, v in d.items()} for m, d in tree.items()}
+
+
+def _assert_tree_close(got, want, rtol, atol):
+    for m in want:
+        for k in want[m]:
+            np.testing.assert_allclose(got[m][k], want[m][k], rtol=rtol, atol=atol, err_msg=f"{m}/{k}")
+
+
+def _assert_moments_close(tr, want_m):
+    """Adam's first moment is linear in the gradients: the gradient check.
+    Tolerance 1e-3 of each leaf's scale (fp32 sums over the minibatch)."""
+    from envmodel.trainer import unflatten
+    got = unflatten(tr._names, tr._shapes, tr.flat(1))
+    for m in want_m:
+        for k in want_m[m]:
+            w = want_m[m][k]
+            np.testing.assert_allclose(got[m][k], w, rtol=1e-3, atol=1e-3 * float(np.abs(w).max()) + 1e-12,
+                                       err_msg=f"m {m}/{k}")
+
+
+def _assert_params_close(got, want, steps, lr=1e-3):
+    """Parameters: Adam normalises each update, so an element whose gradient is
+    ~0 can move by up to lr either way on fp32 vs f64 rounding.  All but 1e-3
+    of the elements within (1e-4 rel, 3e-6 * steps abs); every one within 2 lr
+    per step."""
+    for m in want:
+        for k in want[m]:
+            g, w = np.asarray(got[m][k], np.float64), want[m][k]
+            bad = ~np.isclose(g, w, rtol=1e-4, atol=3e-6 * steps)
+            assert bad.mean() <= 1e-3, (m, k, int(bad.sum()))
+            assert np.abs(g - w).max() <= 2 * lr * steps, (m, k)
+
+
+@pytest.mark.parametrize("tw,shape", [(0.0, (28, 5, (128, 256, 128))), (1.0, (28, 5, (128, 256, 128))),
+                                      (0.0, (42, 8, (64, 96)))])
+def test_state_predictor_steps_match_oracle(tw, shape):
+    D, A, hid = shape
+    spec = em.EnvModelSpec(D, A, hid, (128, 256, 128) if tw > 0 else (64,))
+    rng = np.random.default_rng(0)
+    sp = em.init_state_predictor(spec, 1)
+    sp["LayerNorm_0"]["scale"] = (1 + 0.1 * rng.standard_normal(D + A)).astype(np.float32)
+    sp["LayerNorm_0"]["bias"] = (0.1 * rng.standard_normal(D + A)).astype(np.float32)
+    tp = em.init_termination_predictor(spec, 2)
+    cfg = EnvModelTrainerConfig(steps=50, termination_weight=tw, batch_size=64, init_learning_rate=1e-3)
+    tr = StatePredictorTrainer(spec, sp, None, None, cfg, tp_params=tp if tw > 0 else None)
+    ref, m, v = _f64(sp), T.zeros_like_tree(sp), T.zeros_like_tree(sp)
+    for step in range(3):
+        b = _batch(rng, 64, D, A)
+        _, logs = tr.train_step(None, b)
+        loss, want_logs, grads, _ = T.state_predictor_step(ref, b, tw, 30.0, _f64(tp))
+        for k in logs:
+            assert logs[k] == pytest.approx(want_logs[k], rel=1e-4, abs=1e-7), (step, k)
+        ref, m, v = T.adam_update(ref, grads, m, v, step, T.cosine_lr(1e-3, 50, step))
+        _assert_moments_close(tr, m)
+        _assert_params_close(tr.params, ref, step + 1)
+    assert tr.count == 3
+    # eval_step: logs of the current parameters, no update
+    b = _batch(rng, 64, D, A)
+    logs = tr.eval_step(None, b)
+    _, want_logs, _, _ = T.state_predictor_step(ref, b, tw, 30.0, _f64(tp))
+    assert logs["next_observation_loss"] == pytest.approx(want_logs["next_observation_loss"], rel=1e-4)
+    assert tr.count == 3
+    tr.close()
+
+
+def test_termination_predictor_steps_match_oracle():
+    D = 28
+    spec = em.EnvModelSpec(D, 5, (8,), (128, 256, 128))
+    rng = np.random.default_rng(1)
+    tp = em.init_termination_predictor(spec, 3)
+    cfg = EnvModelTrainerConfig(steps=40, batch_size=128, init_learning_rate=1e-3)
+    tr = TerminationPredictorTrainer(spec, tp, None, None, cfg)
+    ref, m, v = _f64(tp), T.zeros_like_tree(tp), T.zeros_like_tree(tp)
+    keep = rng.uniform(size=(128, D)) >= 0.1
+    for step in range(3):
+        b = _batch(rng, 128, D, 5, p_term=0.3)
+        _, logs = tr.train_step(None, b, keep_mask=keep)
+        loss, want_logs, grads = T.termination_predictor_step(ref, b, keep.astype(np.float64))
+        for k in logs:
+            assert logs[k] == pytest.approx(want_logs[k], rel=1e-4, abs=1e-7), (step, k)
+        ref, m, v = T.adam_update(ref, grads, m, v, step, T.cosine_lr(1e-3, 40, step))
+        _assert_moments_close(tr, m)
+        _assert_params_close(tr.params, ref, step + 1)
+    b = _batch(rng, 128, D, 5, p_term=0.3)
+    logs = tr.eval_step(None, b)
+    want = T.termination_eval_logs(ref, b)
+    for k in ("loss", "true_loss", "false_loss"):
+        assert logs[k] == pytest.approx(want[k], rel=1e-4, abs=1e-7), k
+    for k in ("accuracy", "precision", "recall"):
+        assert logs[k] == pytest.approx(want[k], abs=1.5 / 128), k
+    tr.close()
+
+
+class _Loader:
+    def __init__(self, ds):
+        self.dataset = ds
+
+    def sample(self, n):
+        idx = np.random.randint(len(self.dataset["observations"]), size=n)
+        return {k: v[idx] for k, v in self.dataset.items()}
+
+
+def _dynamics_dataset(n, D, A, seed=0):
+    rng = np.random.default_rng(seed)
+    obs = rng.standard_normal((n, D)).astype(np.float32)
+    act = rng.uniform(-1, 1, (n, A)).astype(np.float32)
+    M = (0.3 * rng.standard_normal((D + A, D))).astype(np.float32)
+    nxt = obs + np.tanh(np.concatenate([obs, act], 1) @ M)
+    return {"observations": obs, "actions": act, "next_observations": nxt.astype(np.float32),
+            "rewards": np.where(nxt[:, 0] > 1.5, 0.0, -1.0).astype(np.float32)}
+
+
+def test_device_sampled_training_learns_and_is_deterministic():
+    D, A = 28, 5
+    spec = em.EnvModelSpec(D, A)
+    ds = _dynamics_dataset(20000, D, A)
+    sp = em.init_state_predictor(spec, 0)
+    cfg = EnvModelTrainerConfig(steps=400, termination_weight=0.0, batch_size=256, seed=5)
+    runs = []
+    for _ in range(2):
+        tr = StatePredictorTrainer(spec, sp, _Loader(dict(ds)), None, cfg)
+        b = {k: v[:256] for k, v in ds.items()}
+        before = tr.eval_step(None, b)["next_observation_loss"]
+        tr.steps(400)
+        after = tr.eval_step(None, b)["next_observation_loss"]
+        runs.append((before, after, tr.flat()))
+        assert tr.count == 400
+        tr.close()
+    assert runs[1][1] < 0.5 * runs[0][0], runs[0][:2]
+    np.testing.assert_array_equal(runs[0][2], runs[1][2])  # same seed -> bit-identical
+    # termination predictor on the same data: loss falls, accuracy above the base rate
+    tp = em.init_termination_predictor(spec, 1)
+    tr = TerminationPredictorTrainer(spec, tp, _Loader(dict(ds)), None,
+                                     EnvModelTrainerConfig(steps=300, batch_size=256, seed=2))
+    b = {k: v[-256:] for k, v in ds.items()}
+    before = tr.eval_step(None, b)["loss"]
+    tr.steps(300)
+    ev = tr.eval_step(None, b)
+    assert ev["loss"] < before
+    base = max(np.mean(b["rewards"] == 0), 1 - np.mean(b["rewards"] == 0))
+    assert ev["accuracy"] >= base - 1e-6
+    tr.close()
+
+
+def test_train_loop_logs_like_reference():
+    D, A = 28, 5
+    spec = em.EnvModelSpec(D, A)
+    ds = _dynamics_dataset(4000, D, A, seed=3)
+
+    class Log:
+        def __init__(self):
+            self.rows = []
+
+        def log(self, d, step):
+            self.rows.append((step, d))
+
+    lg = Log()
+    tr = StatePredictorTrainer(spec, em.init_state_predictor(spec, 0), _Loader(dict(ds)), _Loader(dict(ds)),
+                               EnvModelTrainerConfig(steps=120, termination_weight=0.0, val_batches=2), logger=lg)
+    tr.train()
+    keys = {k for _, d in lg.rows for k in d}
+    assert {"train/loss", "train/next_observation_loss", "val/loss", "val/next_observation_loss"} <= keys
+    assert sorted({s for s, d in lg.rows if "val/loss" in d}) == [0, 100, 120]
+    tr.close()
