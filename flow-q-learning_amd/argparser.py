@@ -61,3 +61,42 @@ def build_config_from_args(args: argparse.Namespace) -> TrainerConfig:
     agent = AgentConfig(**{k: v for k, v in agent_kw.items() if k in AgentConfig.__dataclass_fields__})
     return TrainerConfig(**{k: v for k, v in trainer_kw.items() if k in TrainerConfig.__dataclass_fields__},
                          agent=agent)
+
+
+def get_env_model_argparser() -> argparse.ArgumentParser:
+    """reference argparser.py:172-262 (train_env_model.py's flags)."""
+    p = argparse.ArgumentParser(description="The configurations of the environment model.")
+    p.add_argument("--model", type=str, default="baseline")
+    p.add_argument("--model.hidden_dims", type=literal_eval, default=(128, 256, 128))
+    p.add_argument("--model.latent_dim", type=int, default=4)
+    p.add_argument("--true_termination_weight", type=float, default=30.0)
+    p.add_argument("--termination_weight", type=float, default=1.0)
+    p.add_argument("--reconstruction_weight", type=float, default=1.0)
+    p.add_argument("--sequence_length", type=int, default=256)
+    p.add_argument("--steps", type=int, default=20000)
+    p.add_argument("--env_name", type=str, default="cube-single-play-singletask-task2-v0")
+    p.add_argument("--init_learning_rate", type=float, default=1e-3)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--batch_size", type=int, default=256)
+    p.add_argument("--val_batches", type=int, default=50)
+    p.add_argument("--data_directory", type=str, default="data/")
+    p.add_argument("--save_directory", type=str, default="exp/")
+    return p
+
+
+def build_env_model_config_from_args(args: argparse.Namespace):
+    """reference argparser.py:265-290: --model.* flags into model_config, the rest
+    filtered to the trainer config's fields."""
+    from dataclasses import fields
+
+    from envmodel.trainer import EnvModelTrainerConfig
+    model_config, trainer_kw = {}, {}
+    for k, v in vars(args).items():
+        if k.startswith("model."):
+            model_config[k[len("model."):]] = v
+        else:
+            trainer_kw[k] = v
+    trainer_kw["save_directory"] = Path(trainer_kw["save_directory"])
+    trainer_kw["data_directory"] = Path(trainer_kw["data_directory"])
+    names = {f.name for f in fields(EnvModelTrainerConfig)}
+    return EnvModelTrainerConfig(**{k: v for k, v in trainer_kw.items() if k in names}, model_config=model_config)

@@ -9,6 +9,8 @@ Fixtures
   produced by importing the reference module in a subprocess.
 * ``reference_argparser.json`` -- TrainerConfig built by the REFERENCE
   argparser (reference argparser.py:9-169) for several argv lists.
+* ``reference_env_model_argparser.json`` -- EnvModelTrainerConfig built by the
+  REFERENCE env-model argparser (reference argparser.py:172-290).
 * ``reference_seeds.json``     -- alpha grid / seed draws of reference
   tune_alpha.py:40-46 and the seeds recorded in the reference's
   results/real_success_rates_{cube,antsoccer}.csv.
@@ -63,6 +65,18 @@ for argv in argvs:
     d["save_directory"] = str(d["save_directory"])
     d["data_directory"] = str(d["data_directory"])
     out["argparser"].append({"argv": argv, "config": d})
+out["env_model_argparser"] = []
+em_argvs = [[], ["--model=baseline", "--termination_weight=0"],
+            ["--model=termination_predictor", "--steps=40000"],
+            ["--model=multistep", "--model.hidden_dims=(64, 64)", "--sequence_length=128", "--seed=4",
+             "--env_name=antsoccer-arena-navigate-singletask-task4-v0"]]
+for argv in em_argvs:
+    cfg = argparser.build_env_model_config_from_args(argparser.get_env_model_argparser().parse_args(argv))
+    d = dict(vars(cfg))
+    d["save_directory"] = str(d["save_directory"])
+    d["data_directory"] = str(d["data_directory"])
+    d["model_config"] = {k: list(v) if isinstance(v, tuple) else v for k, v in d["model_config"].items()}
+    out["env_model_argparser"].append({"argv": argv, "config": d})
 print(json.dumps(out))
 '''
 
@@ -74,6 +88,8 @@ def reference_fixtures():
         json.dump(data["hpo"], f)
     with open(os.path.join(HERE, "reference_argparser.json"), "w") as f:
         json.dump(data["argparser"], f, indent=1)
+    with open(os.path.join(HERE, "reference_env_model_argparser.json"), "w") as f:
+        json.dump(data["env_model_argparser"], f, indent=1)
 
     import random
     seeds = {}

@@ -130,3 +130,39 @@ def test_cosine_schedule_and_adam_first_step():
     # first Adam step: -lr * g / (|g| + eps)
     want = 1.0 - 1e-3 * g["Dense_0"]["kernel"] / (np.abs(g["Dense_0"]["kernel"]) + 1e-8)
     np.testing.assert_allclose(nt["Dense_0"]["kernel"], want, rtol=1e-12)
+
+
+def test_env_model_argparser_matches_reference_fixture():
+    """Our get_env_model_argparser / build_env_model_config_from_args against the
+    REFERENCE argparser's output (tests/golden/reference_env_model_argparser.json)."""
+    import json
+
+    import argparser
+    with open(os.path.join(ROOT, "tests", "golden", "reference_env_model_argparser.json")) as f:
+        cases = json.load(f)
+    assert len(cases) >= 4
+    for case in cases:
+        cfg = argparser.build_env_model_config_from_args(argparser.get_env_model_argparser().parse_args(case["argv"]))
+        d = dict(vars(cfg))
+        d["save_directory"] = str(d["save_directory"])
+        d["data_directory"] = str(d["data_directory"])
+        d["model_config"] = {k: list(v) if isinstance(v, tuple) else v for k, v in d["model_config"].items()}
+        assert d == case["config"], case["argv"]
+
+
+def test_trainer_flat_layout_roundtrip():
+    from envmodel.trainer import _leaf_shapes, unflatten
+    spec = em.EnvModelSpec(28, 5)
+    sp = em.init_state_predictor(spec, 0)
+    flat = em.flatten_state_predictor(spec, sp)
+    names = em.sp_leaf_names(spec)
+    tree = unflatten(names, _leaf_shapes(names, spec.sp_dims(), 33), flat)
+    for m in sp:
+        for k in sp[m]:
+            np.testing.assert_array_equal(tree[m][k], sp[m][k])
+    tp = em.init_termination_predictor(spec, 1)
+    names = em.tp_leaf_names(spec)
+    tree = unflatten(names, _leaf_shapes(names, spec.tp_dims()), em.flatten_termination_predictor(spec, tp))
+    for m in tp:
+        for k in tp[m]:
+            np.testing.assert_array_equal(tree[m][k], tp[m][k])

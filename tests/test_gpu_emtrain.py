@@ -185,3 +185,25 @@ def test_train_loop_logs_like_reference():
     assert {"train/loss", "train/next_observation_loss", "val/loss", "val/next_observation_loss"} <= keys
     assert sorted({s for s, d in lg.rows if "val/loss" in d}) == [0, 100, 120]
     tr.close()
+
+
+def test_train_env_model_driver(tmp_path):
+    """train_env_model.py end to end on a synthetic .npz: termination predictor, then the
+    baseline with termination_weight > 0 loading it, saved flax-msgpack params readable back."""
+    import train_env_model as tem
+    D, A = 28, 5
+    ds = _dynamics_dataset(3000, D, A, seed=9)
+    data = tmp_path / "data"
+    data.mkdir()
+    np.savez(data / "cube-single-play.npz", observations=ds["observations"], actions=ds["actions"],
+             next_observations=ds["next_observations"], rewards=ds["rewards"])
+    common = [f"--data_directory={data}", f"--save_directory={tmp_path / 'exp'}", "--val_batches=2"]
+    out = tem.main(["--model=termination_predictor", "--steps=150"] + common)
+    tp = em.load_flax_msgpack(out / "termination_predictor.pt")["params"]
+    assert tp["Dense_0"]["kernel"].shape == (D, 128)
+    out = tem.main(["--model=baseline", "--steps=150", "--termination_weight=1"] + common)
+    sp = em.load_flax_msgpack(out / "baseline.pt")["params"]
+    assert sp["LayerNorm_0"]["scale"].shape == (D + A,)
+    assert (out / "baseline_config.yaml").exists() and (out / "baseline_log.csv").exists()
+    with pytest.raises(ValueError):
+        tem.main(["--model=multistep", "--steps=10"] + common)
