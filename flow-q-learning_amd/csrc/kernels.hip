@@ -734,9 +734,10 @@ DEV float gelu_grad_fast(float x) {
 // k < 4 NS (NS a multiple of EF_PF).  ring[] holds the next EF_PF k-steps' A
 // fragments on entry; on exit it holds the first EF_PF of the layer at
 // w_next (element offset of the next layer's Dense kernel).
-DEV void ef_kloop(f32x4 (&acc)[4], float4 (&ring)[EF_PF], rsrc_t rW, const float* xs, int NS, int w_cur,
+template <int PF = EF_PF>
+DEV void ef_kloop(f32x4 (&acc)[4], float4 (&ring)[PF], rsrc_t rW, const float* xs, int NS, int w_cur,
                   int w_next, int lo, int lk, int li) {
-    constexpr int H = EF_H, NC = EF_NC, PF = EF_PF;
+    constexpr int H = EF_H, NC = EF_NC;
     float bnext = xs[lk * NC + li];
     for (int s0 = 0; s0 < NS; s0 += PF) {
         // refill targets: k-steps s0+PF.. of this layer, or the next layer's first PF
@@ -1476,7 +1477,10 @@ void launch_input_grad(const InGradArgs& a, hipStream_t s) {
 // MFMA c of k-step s, whose reduction slot lk is j = 16s + 4lk + c).  In this
 // layout the LayerNorm column statistics take one 16-lane DPP row sum and the
 // per-feature sums over the block's columns (parameter grads) two shuffles.
-constexpr int SB_PF = 8;    // float4 W^T loads in flight per lane (as ef_kloop)
+// float4 W^T loads in flight per lane: the LN (critic) kernel runs 2 blocks per CU
+// (1024 blocks; <= 128 VGPRs), whose other block hides what a 4-deep ring does not;
+// the one-step / BC kernels (256 blocks, 1 per CU) keep the 8-deep ring
+template <bool LN> constexpr int sb_pf() { return LN ? 4 : 8; }
 
 template <int CTRL>
 DEV float dpp_mov(float v) {
@@ -1504,8 +1508,8 @@ bool stream_bwd_supported(int H, int L, int nout, int M, int Mg) {
 }
 
 template <bool LN>
-__global__ __launch_bounds__(EF_NW * 64, 1) void stream_bwd_kernel(const StreamBwdArgs g) {
-    constexpr int H = EF_H, NC = EF_NC, NT = EF_NW * 64, PF = SB_PF;
+__global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(const StreamBwdArgs g) {
+    constexpr int H = EF_H, NC = EF_NC, NT = EF_NW * 64, PF = sb_pf<LN>();
     __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];  // du_l [H][NC] (+ look-ahead slack)
     __shared__ __attribute__((aligned(16))) float scr[H * NC];         // head kernel W_L [H][nout]; then LN-grad products
     __shared__ float colred[2][EF_NW][NC];                            // LN column-stat partials per wave
@@ -1697,7 +1701,7 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_bwd_kernel(const StreamB
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int wn = (int)g.wt_off[l >= 2 ? l - 1 : l];  // next product's W^T (l-1 >= 1), else a harmless re-load
-        ef_kloop(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lo, lk, li);
+        ef_kloop<PF>(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lo, lk, li);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
