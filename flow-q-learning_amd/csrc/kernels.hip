@@ -190,6 +190,7 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
     float* __restrict__ Tt = e.target ? e.target + (long long)slot * e.PT + e.w_off[gi] + (long long)y * e.ens : nullptr;
     const float t = (float)(e.count[slot] + 1);
     const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
+    const float rbc1 = 1.0f / bc1, rbc2 = 1.0f / bc2;
     const float lr = e.lr, tau = e.tau;
     float mx = -INFINITY, mn = INFINITY, ss = 0.f;
     const int rows = e.mode == 1 ? 0 : min(BM, gM - i0);  // mode 1: timing probe only (no optimiser traffic)
@@ -224,9 +225,11 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
                     const float gr = gs[c];
                     mm[c] = 0.1f * gr + 0.9f * mm[c];
                     vv[c] = 0.001f * (gr * gr) + 0.999f * vv[c];
-                    const float mh = mm[c] / bc1, vh = vv[c] / bc2;
+                    // bias corrections by reciprocal and the step by v_sqrt + v_rcp: <= 2 ulp from
+                    // optax's IEEE divisions, and 3 IEEE division sequences fewer per element
+                    const float mh = mm[c] * rbc1, vh = vv[c] * rbc2;
                     tt[c] = tau * pp[c] + (1.0f - tau) * tt[c];
-                    pp[c] = pp[c] + (-lr) * (mh / (sqrtf(vh) + 1e-8f));
+                    pp[c] = pp[c] + (-lr) * (mh * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vh) + 1e-8f));
                     gs[c] = pp[c];
                     mx = fmaxf(mx, gr);
                     mn = fminf(mn, gr);
