@@ -51,6 +51,24 @@ void launch_gemm_variant(int layout, int epi, int tile, int variant, const GemmA
 // Up to GEMM_GROUP_MAX independent dW-layout problems (A and B both
 // r-contiguous, EPI_STORE) in one launch; N % BN == 0 for every problem.
 constexpr int GEMM_GROUP_MAX = 8;
+struct Chunk { long long off; int len; int leaf; };  // element offset into a net's param block
+struct AdamArgs {
+    const float* p_in;            // parameters read (current buffer, slot stride P)
+    float* p_out;                 // parameters written (the other buffer of the pair)
+    float *g, *m, *v;             // arenas (slot stride P)
+    float* target;                // target arena (slot stride PT) or null
+    long long P, PT;
+    long long net_off;            // offset of this net inside the params arena
+    const Chunk* chunks;          // chunk table of ALL nets (index = stats chunk id)
+    const int* ids;               // chunk ids to process (block = ids[blockIdx.x]), or null:
+    int n_chunks, chunk_base;     //   chunk ids chunk_base .. chunk_base + n_chunks - 1
+    float* stats;                 // [slots][n_total_chunks][3] (max, min, sumsq)
+    int n_total_chunks;
+    const int* count;
+    float lr, tau;
+    int nz;
+    const int* slots;
+};
 // Fused optimiser epilogue of the grouped dW launch: problem gi is the kernel
 // leaf W_l of one net; its output tile is the gradient, and the epilogue runs
 // optax.adam on it (reading p from p_in, writing p_out, m, v in place), the
@@ -70,6 +88,10 @@ struct AdamEpi {
     const int* count;
     float lr, tau;
     int mode;                         // 0; timing probes (FQLPOP_DW_MODE): 1 = no optimiser pass, 2 = one k-slice
+    // the net's small leaves (biases, LN, head) ride in the same launch: blocks past the
+    // GEMM tiles run the adam_kernel body on small.ids chunks (small_blocks = chunks x nz)
+    AdamArgs small;
+    int small_blocks;
 };
 struct GemmGroupArgs {
     GemmArgs g[GEMM_GROUP_MAX];
@@ -296,24 +318,6 @@ void launch_loss_bc(const LossArgs& a, hipStream_t s);
 void launch_loss_actor(const LossArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------- optimiser ----
-struct Chunk { long long off; int len; int leaf; };  // element offset into a net's param block
-struct AdamArgs {
-    const float* p_in;            // parameters read (current buffer, slot stride P)
-    float* p_out;                 // parameters written (the other buffer of the pair)
-    float *g, *m, *v;             // arenas (slot stride P)
-    float* target;                // target arena (slot stride PT) or null
-    long long P, PT;
-    long long net_off;            // offset of this net inside the params arena
-    const Chunk* chunks;          // chunk table of ALL nets (index = stats chunk id)
-    const int* ids;               // chunk ids to process (block = ids[blockIdx.x]), or null:
-    int n_chunks, chunk_base;     //   chunk ids chunk_base .. chunk_base + n_chunks - 1
-    float* stats;                 // [slots][n_total_chunks][3] (max, min, sumsq)
-    int n_total_chunks;
-    const int* count;
-    float lr, tau;
-    int nz;
-    const int* slots;
-};
 void launch_adam(const AdamArgs& a, hipStream_t s);
 
 struct FinalArgs {

@@ -91,6 +91,80 @@ DEV int xcd_remap(int bid, int total) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
 }
 
+// optax.adam (b1 .9, b2 .999, eps 1e-8 outside the sqrt, bias correction with
+// count+1) + target EMA from the pre-update critic + per-chunk grad stats, one
+// chunk of one member per 256-thread block (adam_kernel; and the small-leaf
+// blocks of the fused dW launch).
+DEV void adam_chunk(const AdamArgs& a, int bx, int z) {
+    const int ci = a.ids ? a.ids[bx] : a.chunk_base + bx;
+    const int slot = a.slots[z];
+    const Chunk ck = a.chunks[ci];
+    const long long base = (long long)slot * a.P + a.net_off + ck.off;
+    const float* __restrict__ Pin = a.p_in + base;
+    float* __restrict__ P = a.p_out + base;
+    const float* __restrict__ G = a.g + base;
+    float* __restrict__ Mm = a.m + base;
+    float* __restrict__ V = a.v + base;
+    float* __restrict__ T = a.target ? a.target + (long long)slot * a.PT + ck.off : nullptr;
+    const float t = (float)(a.count[slot] + 1);
+    const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
+    float mx = -INFINITY, mn = INFINITY, ss = 0.f;
+    const float lr = a.lr, tau = a.tau;
+    // one Adam element (+ EMA of the target from the pre-update value)
+#define FQ_ADAM1(g, p, m, v, hasT, tp)                              \
+    do {                                                            \
+        m = 0.1f * (g) + 0.9f * m;                                  \
+        v = 0.001f * ((g) * (g)) + 0.999f * v;                      \
+        const float mh_ = m / bc1, vh_ = v / bc2;                   \
+        if (hasT) tp = tau * p + (1.0f - tau) * tp;                 \
+        p = p + (-lr) * (mh_ / (sqrtf(vh_) + 1e-8f));               \
+        mx = fmaxf(mx, (g));                                        \
+        mn = fminf(mn, (g));                                        \
+        ss += (g) * (g);                                            \
+    } while (0)
+    const bool hasT = T != nullptr;
+    if ((ck.len & 3) == 0) {
+        for (int i = threadIdx.x * 4; i < ck.len; i += 1024) {
+            const float4 g4 = *reinterpret_cast<const float4*>(G + i);
+            float4 p4 = *reinterpret_cast<const float4*>(Pin + i);
+            float4 m4 = *reinterpret_cast<float4*>(Mm + i);
+            float4 v4 = *reinterpret_cast<float4*>(V + i);
+            float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (hasT) t4 = *reinterpret_cast<float4*>(T + i);
+            FQ_ADAM1(g4.x, p4.x, m4.x, v4.x, hasT, t4.x);
+            FQ_ADAM1(g4.y, p4.y, m4.y, v4.y, hasT, t4.y);
+            FQ_ADAM1(g4.z, p4.z, m4.z, v4.z, hasT, t4.z);
+            FQ_ADAM1(g4.w, p4.w, m4.w, v4.w, hasT, t4.w);
+            *reinterpret_cast<float4*>(P + i) = p4;
+            *reinterpret_cast<float4*>(Mm + i) = m4;
+            *reinterpret_cast<float4*>(V + i) = v4;
+            if (hasT) *reinterpret_cast<float4*>(T + i) = t4;
+        }
+    } else {
+        for (int i = threadIdx.x; i < ck.len; i += 256) {
+            const float gv = G[i];
+            float p = Pin[i], m = Mm[i], v = V[i], tv = hasT ? T[i] : 0.f;
+            FQ_ADAM1(gv, p, m, v, hasT, tv);
+            P[i] = p;
+            Mm[i] = m;
+            V[i] = v;
+            if (hasT) T[i] = tv;
+        }
+    }
+#undef FQ_ADAM1
+    __shared__ float red[4];
+    mx = block_max(mx, red);
+    mn = block_min(mn, red);
+    ss = block_sum(ss, red);
+    if (threadIdx.x == 0) {
+        float* st = a.stats + ((long long)slot * a.n_total_chunks + ci) * 3;
+        st[0] = mx;
+        st[1] = mn;
+        st[2] = ss;
+    }
+}
+
+
 // =============================================================== GEMM ======
 // C[i][j] = sum_r A(i,r) B(r,j) over one (member, ensemble) pair per block
 // tile.  256 threads = 4 waves in a 2x2 grid; each wave owns (BM/2)x(BN/2)
@@ -434,6 +508,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
 template <int BM, int BN, bool ARC, bool BRC, int EPI = EPI_STORE>
 __global__ __launch_bounds__(256, 2) void gemm_group_kernel(const GemmGroupArgs ga) {
     __shared__ __attribute__((aligned(16))) float smem[gemm_smem_floats<BM, BN, 32, ARC, BRC>()];
+    if (EPI == EPI_ADAM && (int)blockIdx.x >= ga.first[ga.ng]) {
+        // the net's small leaves: raw block ids past the tiles (the dispatcher spreads
+        // consecutive ids over the XCDs, so they add no per-XCD imbalance)
+        const int sb = blockIdx.x - ga.first[ga.ng], nch = ga.adam.small.n_chunks;
+        adam_chunk(ga.adam.small, sb % nch, sb / nch);
+        return;
+    }
     const int bid = xcd_remap(blockIdx.x, ga.first[ga.ng]);
     int gi = 0;
 #pragma unroll
@@ -459,6 +540,7 @@ void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, c
     ga.ng = ng;
     if (adam) {
         ga.adam = *adam;
+        tot += adam->small_blocks;
         switch (tile) {
             case 0: hipLaunchKernelGGL((gemm_group_kernel<64, 64, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga); break;
             case 1: hipLaunchKernelGGL((gemm_group_kernel<128, 64, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga); break;
@@ -2101,74 +2183,7 @@ void launch_loss_actor(const LossArgs& a, hipStream_t s) {
 // optax.adam(lr) (b1 .9, b2 .999, eps 1e-8 outside the sqrt, bias correction
 // with count+1) fused with the target-critic EMA (from the PRE-update critic)
 // and the per-chunk grad statistics of apply_loss_fn (max, min, sum g^2).
-__global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) {
-    const int ci = a.ids ? a.ids[blockIdx.x] : a.chunk_base + blockIdx.x, z = blockIdx.y;
-    const int slot = a.slots[z];
-    const Chunk ck = a.chunks[ci];
-    const long long base = (long long)slot * a.P + a.net_off + ck.off;
-    const float* __restrict__ Pin = a.p_in + base;
-    float* __restrict__ P = a.p_out + base;
-    const float* __restrict__ G = a.g + base;
-    float* __restrict__ Mm = a.m + base;
-    float* __restrict__ V = a.v + base;
-    float* __restrict__ T = a.target ? a.target + (long long)slot * a.PT + ck.off : nullptr;
-    const float t = (float)(a.count[slot] + 1);
-    const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
-    float mx = -INFINITY, mn = INFINITY, ss = 0.f;
-    const float lr = a.lr, tau = a.tau;
-    // one Adam element (+ EMA of the target from the pre-update value)
-#define FQ_ADAM1(g, p, m, v, hasT, tp)                              \
-    do {                                                            \
-        m = 0.1f * (g) + 0.9f * m;                                  \
-        v = 0.001f * ((g) * (g)) + 0.999f * v;                      \
-        const float mh_ = m / bc1, vh_ = v / bc2;                   \
-        if (hasT) tp = tau * p + (1.0f - tau) * tp;                 \
-        p = p + (-lr) * (mh_ / (sqrtf(vh_) + 1e-8f));               \
-        mx = fmaxf(mx, (g));                                        \
-        mn = fminf(mn, (g));                                        \
-        ss += (g) * (g);                                            \
-    } while (0)
-    const bool hasT = T != nullptr;
-    if ((ck.len & 3) == 0) {
-        for (int i = threadIdx.x * 4; i < ck.len; i += 1024) {
-            const float4 g4 = *reinterpret_cast<const float4*>(G + i);
-            float4 p4 = *reinterpret_cast<const float4*>(Pin + i);
-            float4 m4 = *reinterpret_cast<float4*>(Mm + i);
-            float4 v4 = *reinterpret_cast<float4*>(V + i);
-            float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (hasT) t4 = *reinterpret_cast<float4*>(T + i);
-            FQ_ADAM1(g4.x, p4.x, m4.x, v4.x, hasT, t4.x);
-            FQ_ADAM1(g4.y, p4.y, m4.y, v4.y, hasT, t4.y);
-            FQ_ADAM1(g4.z, p4.z, m4.z, v4.z, hasT, t4.z);
-            FQ_ADAM1(g4.w, p4.w, m4.w, v4.w, hasT, t4.w);
-            *reinterpret_cast<float4*>(P + i) = p4;
-            *reinterpret_cast<float4*>(Mm + i) = m4;
-            *reinterpret_cast<float4*>(V + i) = v4;
-            if (hasT) *reinterpret_cast<float4*>(T + i) = t4;
-        }
-    } else {
-        for (int i = threadIdx.x; i < ck.len; i += 256) {
-            const float gv = G[i];
-            float p = Pin[i], m = Mm[i], v = V[i], tv = hasT ? T[i] : 0.f;
-            FQ_ADAM1(gv, p, m, v, hasT, tv);
-            P[i] = p;
-            Mm[i] = m;
-            V[i] = v;
-            if (hasT) T[i] = tv;
-        }
-    }
-#undef FQ_ADAM1
-    __shared__ float red[4];
-    mx = block_max(mx, red);
-    mn = block_min(mn, red);
-    ss = block_sum(ss, red);
-    if (threadIdx.x == 0) {
-        float* st = a.stats + ((long long)slot * a.n_total_chunks + ci) * 3;
-        st[0] = mx;
-        st[1] = mn;
-        st[2] = ss;
-    }
-}
+__global__ __launch_bounds__(256) void adam_kernel(const AdamArgs a) { adam_chunk(a, blockIdx.x, blockIdx.y); }
 
 void launch_adam(const AdamArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(adam_kernel, dim3(a.n_chunks, a.nz), dim3(256), 0, s, a);

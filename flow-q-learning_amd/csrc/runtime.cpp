@@ -565,6 +565,8 @@ void bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_
     }
 }
 
+AdamArgs adam_args(const Ctx& c, int ni);
+
 // Whole-network backward of `N` (stream_bwd_kernel) on `s`: dX chain from the
 // head gradient `dout` ([nout][ld_o]) down to du_0, LayerNorm / GELU' fused,
 // parameter-grad column sums as per-tile partials.  Then, on `sw`, the
@@ -668,6 +670,8 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
             const char* dm = std::getenv("FQLPOP_DW_MODE");
             ae.mode = dm ? std::atoi(dm) : 0;
         }
+        ae.small = adam_args(c, ni);
+        ae.small_blocks = ae.small.n_chunks * c.nz;
         launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw, &ae);
     } else if (N.L <= GEMM_GROUP_MAX && N.H % 128 == 0) {
         launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw);
@@ -707,9 +711,7 @@ void transpose_nets(fqlpop* h, hipStream_t s, int mask, bool all_slots, const fl
     launch_transpose(t, s);
 }
 
-// Adam (+ EMA, grad stats) of net ni from params to params_nx: every leaf, or
-// with the fused optimiser only the leaves the dW epilogue does not cover.
-void adam_net(const Ctx& c, hipStream_t s, int ni) {
+AdamArgs adam_args(const Ctx& c, int ni) {
     fqlpop* h = c.h;
     const NetLayout* nets[3] = {&h->critic, &h->bc, &h->os};
     AdamArgs a{};
@@ -727,12 +729,19 @@ void adam_net(const Ctx& c, hipStream_t s, int ni) {
         a.n_chunks = h->n_chunks_net[ni];
         a.chunk_base = h->chunk_base_net[ni];
     }
-    if (a.n_chunks == 0) return;
     a.stats = h->stats; a.n_total_chunks = h->n_chunks_total;
     a.count = h->count;
     a.lr = h->cfg.lr; a.tau = h->cfg.tau;
     a.nz = c.nz; a.slots = h->slots;
-    launch_adam(a, s);
+    return a;
+}
+
+// Adam (+ EMA, grad stats) of net ni from params to params_nx: every leaf, or
+// with the fused optimiser only the leaves the dW epilogue does not cover
+// (those normally ride in the fused launch itself, see stream_bwd_net).
+void adam_net(const Ctx& c, hipStream_t s, int ni) {
+    const AdamArgs a = adam_args(c, ni);
+    if (a.n_chunks > 0) launch_adam(a, s);
 }
 
 // One whole-network forward launch (stream_fwd_kernel).  `arena` + N.off is the
@@ -922,8 +931,10 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         else
             bwd_net(c, sB, N, tref(h->dv, (long long)A * B), B, tref(h->bc_in, (long long)Kb * B2), B2, 0, B, B,
                     h->bc_u, h->bc_g, 0, nullptr, nullptr, 0, h->bc_du, h->bc_dh, nullptr, nullptr, B, sB);
-        adam_net(c, sB, 1);
-        if (h->stream_bwd && !h->fused_adam) transpose_nets(h, sB, 2, false, h->params_nx, h->paramsT_nx);
+        if (!h->fused_adam) {
+            adam_net(c, sB, 1);
+            if (h->stream_bwd) transpose_nets(h, sB, 2, false, h->params_nx, h->paramsT_nx);
+        }
     }
     HIPCHK(hipEventRecord(h->ev_bdone, sB));
 
@@ -1045,10 +1056,8 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3,
                            B, B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, B, h->part_os, sM, nullptr,
                            &os_dw);
-            critic_dw();
-            adam_net(c, sX, 0);
+            critic_dw();  // the fused launches include each net's small-leaf Adam
             os_dw();
-            adam_net(c, sM, 2);
         } else if (h->stream_bwd)
             stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3,
                            B, B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, B, h->part_os, sX);
