@@ -2190,43 +2190,49 @@ void launch_adam(const AdamArgs& a, hipStream_t s) {
 }
 
 // grad/max, grad/min over every leaf (target-critic leaves contribute zeros),
-// grad/norm = sum over leaves of the leaf L2 norm; count += 1.  Thread = leaf
-// (its chunks in order), then fixed-pattern reductions: deterministic.
-__global__ __launch_bounds__(128) void finalize_kernel(const FinalArgs a) {
+// grad/norm = sum over leaves of the leaf L2 norm; count += 1.  Wave = leaf
+// (leaves w, w + 16, ...): lanes stride its chunks, wave reductions, then thread
+// 0 folds the leaves in order -- fixed pattern, deterministic.
+constexpr int FIN_WAVES = 16;
+__global__ __launch_bounds__(FIN_WAVES * 64) void finalize_kernel(const FinalArgs a) {
     const int z = blockIdx.x, slot = a.slots[z];
-    const int t = threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const float* st = a.stats + (long long)slot * a.n_total_chunks * 3;
-    float mx = 0.f, mn = 0.f, nrm = 0.f;  // zero target-critic leaves are part of the tree
-    if (t < a.n_leaves) {
-        float ss = 0.f;
-        for (int c = a.leaf_first[t]; c < a.leaf_first[t + 1]; ++c) {
+    __shared__ float leaf[3][128];
+    for (int l = w; l < a.n_leaves; l += FIN_WAVES) {
+        float mx = -INFINITY, mn = INFINITY, ss = 0.f;
+        for (int c = a.leaf_first[l] + lane; c < a.leaf_first[l + 1]; c += 64) {
             mx = fmaxf(mx, st[c * 3 + 0]);
             mn = fminf(mn, st[c * 3 + 1]);
             ss += st[c * 3 + 2];
         }
-        nrm = sqrtf(ss);
-    }
-    __shared__ float red[3][2];
-    mx = wave_max(mx);
-    mn = wave_min(mn);
-    nrm = wave_sum(nrm);
-    if ((t & 63) == 0) {
-        red[0][t >> 6] = mx;
-        red[1][t >> 6] = mn;
-        red[2][t >> 6] = nrm;
+        mx = wave_max(mx);
+        mn = wave_min(mn);
+        ss = wave_sum(ss);
+        if (lane == 0) {
+            leaf[0][l] = mx;
+            leaf[1][l] = mn;
+            leaf[2][l] = sqrtf(ss);
+        }
     }
     __syncthreads();
-    if (t == 0) {
+    if (threadIdx.x == 0) {
+        float mx = 0.f, mn = 0.f, nrm = 0.f;  // zero target-critic leaves are part of the tree
+        for (int l = 0; l < a.n_leaves; ++l) {
+            mx = fmaxf(mx, leaf[0][l]);
+            mn = fminf(mn, leaf[1][l]);
+            nrm += leaf[2][l];
+        }
         float* info = at(a.info, slot);
-        info[10] = fmaxf(red[0][0], red[0][1]);
-        info[11] = fminf(red[1][0], red[1][1]);
-        info[12] = red[2][0] + red[2][1];
+        info[10] = mx;
+        info[11] = mn;
+        info[12] = nrm;
         a.count[slot] += 1;
     }
 }
 
 void launch_finalize(const FinalArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(a.nz), dim3(128), 0, s, a);
+    hipLaunchKernelGGL(finalize_kernel, dim3(a.nz), dim3(FIN_WAVES * 64), 0, s, a);
 }
 
 // ================================================================= init ====
