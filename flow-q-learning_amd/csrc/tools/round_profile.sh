@@ -12,7 +12,7 @@ timeout -k 10 400 python "$R/bench.py" > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.
 timeout -k 10 300 python "$R/bench.py" --no-probe --no-cpu-baseline > "$O/bench_${TAG}_noprobe.json" 2>> "$O/bench_$TAG.err"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o run -- \
-    python3 "$R/bench.py" --steps 100 --warmup 20 --no-cpu-baseline --kernel-iters 1 > "$O/prof_$TAG.log" 2>&1
+    python3 "$R/bench.py" --steps 100 --warmup 20 --no-cpu-baseline --kernel-iters 1 --envmodel-train-steps 0 > "$O/prof_$TAG.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" --output-format csv -d "$O/pmcf_$TAG" -o run -- \
     python3 "$R/flow-q-learning_amd/csrc/tools/profile_dominant.py" 20 > "$O/pmcf_$TAG.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" --output-format csv -d "$O/pmcw_$TAG" -o run -- \
