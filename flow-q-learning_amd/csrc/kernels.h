@@ -212,6 +212,11 @@ struct StreamBwdArgs {
     float* part;                          // [slot][y][tile < Mg/16][NP]
     int NP;
     int L, M, Mg, nout;
+    // optional (critic): dQ/da of the actor's action inputs for the columns [Mg, M),
+    // da[slot][y][j][m - Mg] = sum_f W_0[D0 + j][f] du_0[f][m], one partial per ensemble member
+    float* da;
+    long long da_ss, da_sy;
+    int ld_da, D0, na;
     int ny, nz;
     const int* slots;
 };
@@ -300,14 +305,14 @@ void launch_sample(const SampleArgs& a, hipStream_t s);
 struct LossArgs {
     TRef q, qt, rew, mask;        // q'[E][2B], qt'[E][B]
     TRef vpred, act, x0, amet;    // [A][B]
-    TRef apiraw, aflow, da;       // [A][B]
+    TRef apiraw, aflow, da;       // [A][B]; da: da_n partials at ensemble stride da.sy, summed
     TRef dq;                      // out [E][2B]
     TRef dv;                      // out [A][B]
     TRef dout_os;                 // out [A][B]
     TRef g_cb4, g_bcb4, g_osb4;   // head-bias grads: critic [E] (ens stride), bc [A], os [A]
     TRef info;                    // [16]
     const float* alpha;           // per slot
-    int B, A, E;
+    int B, A, E, da_n;
     int q_min, normq;
     float discount;
     int nz;

@@ -1778,6 +1778,22 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         }
         __syncthreads();
         if (gp) part[l * H + tid] = row_sum(slab);  // bias: sum du
+        if (l == 0 && g.da != nullptr && !gp) {
+            // dQ/da for the actor's Q-loss columns (replaces input_grad_kernel): output (j, col)
+            // = thread & 127, feature quarter = thread >> 7, then a fixed-order fold in scr
+            const int o = tid & 127, q = tid >> 7, j = o >> 4, col = o & 15;
+            float s = 0.f;
+            if (j < g.na) {
+                const float* __restrict__ wr = P + g.w_off[0] + (long long)(g.D0 + j) * H;
+#pragma unroll 8
+                for (int f = q * (H / 4); f < (q + 1) * (H / 4); ++f) s = fmaf(wr[f], slab[f * NC + col], s);
+            }
+            scr[q * 128 + o] = s;
+            __syncthreads();
+            if (tid < g.na * NC)
+                g.da[(long long)slot * g.da_ss + (long long)y * g.da_sy + (long long)(tid >> 4) * g.ld_da +
+                     (c0 - g.Mg) + (tid & 15)] = scr[tid] + scr[128 + tid] + scr[256 + tid] + scr[384 + tid];
+        }
         if (l == 0) break;
 
         // ---- dh_{l-1} = W_l du_l = (W_l^T)^T du_l: the forward k-loop on W_l^T ----
@@ -2136,6 +2152,8 @@ __global__ __launch_bounds__(256) void loss_actor_kernel(const LossArgs a) {
     const float* ap = at(a.apiraw, slot);
     const float* af = at(a.aflow, slot);
     const float* da = at(a.da, slot);
+    const long long da_sy = a.da.sy;
+    const int da_n = a.da_n;
     float* dout = at(a.dout_os, slot);
     const float sc = 2.0f / (float)(A * B);
     float s = 0.f;
@@ -2150,7 +2168,9 @@ __global__ __launch_bounds__(256) void loss_actor_kernel(const LossArgs a) {
                 const float x = ap[o];
                 const float d = x - af[o];
                 s += d * d;
-                const float g = alpha * (sc * d) + ((x > -1.0f && x < 1.0f) ? da[o] : 0.0f);
+                float dq = da[o];
+                for (int e = 1; e < da_n; ++e) dq += da[e * da_sy + o];
+                const float g = alpha * (sc * d) + ((x > -1.0f && x < 1.0f) ? dq : 0.0f);
                 dout[o] = g;
                 sdb[j] += g;
             }

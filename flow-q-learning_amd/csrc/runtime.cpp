@@ -611,9 +611,13 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
     a.part = part; a.NP = stream_bwd_np(N.L, N.H, N.out_dim, N.ln);
     a.L = N.L; a.M = M; a.Mg = Mg; a.nout = N.out_dim;
     a.ny = N.E; a.nz = c.nz; a.slots = h->slots;
+    if (ig) {
+        // the critic's dQ/da, computed by the backward's layer-0 epilogue (per-ensemble partials)
+        ARGCHK(ig->off == Mg && ig->M == M - Mg, "input-grad columns must follow the grad columns");
+        a.da = ig->da.p; a.da_ss = ig->da.ss; a.da_sy = (long long)ig->A * ig->M;
+        a.ld_da = ig->M; a.D0 = ig->D; a.na = ig->A;
+    }
     launch_stream_bwd(N.ln, a, s);
-    // the critic's dQ/da goes first: the actor chain waits for it, not for the dW
-    if (ig) launch_input_grad(*ig, s);
     hipEvent_t ev = nullptr;
     if (sw != s) {
         ev = next_event(h);
@@ -860,7 +864,8 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     la.amet = tref(h->amet, (long long)A * B);
     la.apiraw = tref(h->apiraw, (long long)A * B);
     la.aflow = tref(h->aflow, (long long)A * B);
-    la.da = tref(h->da, (long long)A * B);
+    la.da = tref(h->da, (long long)E * A * B, (long long)A * B);
+    la.da_n = h->stream_bwd ? E : 1;  // per-ensemble partials of the streamed backward, else one sum
     la.dq = tref(h->dq, (long long)E * B2, B2);
     la.dv = tref(h->dv, (long long)A * B);
     la.dout_os = tref(h->dout_os, (long long)A * B);
@@ -1025,7 +1030,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         InGradArgs ig{};
         ig.W0 = pref(h, h->params, NC, NC.W[0]);
         ig.du0 = tref(h->cr_du[0], (long long)H * B2 * E, sy2);
-        ig.da = tref(h->da, (long long)A * B);
+        ig.da = tref(h->da, (long long)E * A * B);
         ig.H = H; ig.D = D; ig.A = A; ig.E = E; ig.ld = B2; ig.off = B; ig.M = B;
         ig.nz = c.nz; ig.slots = h->slots;
         if (h->stream_bwd) {
@@ -1385,9 +1390,9 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         h->q = h->alloc((long long)E * B2);
         h->dq = h->alloc((long long)E * B2);
         h->qt = h->alloc((long long)E * B);
-        for (float** p : {&h->vpred, &h->dv, &h->act_t, &h->x0_t, &h->apiraw, &h->aflow, &h->amet, &h->da,
-                          &h->dout_os})
+        for (float** p : {&h->vpred, &h->dv, &h->act_t, &h->x0_t, &h->apiraw, &h->aflow, &h->amet, &h->dout_os})
             *p = h->alloc((long long)A * B);
+        h->da = h->alloc((long long)E * A * B);  // dQ/da, one partial per critic ensemble member
         h->rew_t = h->alloc(B);
         h->mask_t = h->alloc(B);
         h->info = h->alloc(FQLPOP_INFO_STRIDE);
