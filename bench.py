@@ -144,23 +144,30 @@ def envmodel_train_leg(wl: dict, data: dict, steps: int) -> dict:
     spec = em.EnvModelSpec(wl["obs_dim"], wl["action_dim"])
     ds = {k: data[k] for k in ("observations", "actions", "rewards", "next_observations")}
     out = {}
-    for name, cls, params, cfg in (
+    ms_steps = max(10, steps // 20)
+    for name, cls, params, cfg, n in (
             ("state_predictor", StatePredictorTrainer, em.init_state_predictor(spec, 0),
-             EnvModelTrainerConfig(steps=steps, termination_weight=0.0)),
+             EnvModelTrainerConfig(steps=steps, termination_weight=0.0), steps),
             ("termination_predictor", TerminationPredictorTrainer, em.init_termination_predictor(spec, 1),
-             EnvModelTrainerConfig(steps=steps))):
-        tr = cls(spec, params, _Loader(ds), None, cfg)
-        tr.steps(20)
+             EnvModelTrainerConfig(steps=steps), steps),
+            ("multistep_T256", StatePredictorTrainer, em.init_state_predictor(spec, 0),
+             EnvModelTrainerConfig(steps=ms_steps, model="multistep", sequence_length=256,
+                                   termination_weight=0.0), ms_steps)):
+        n_ep = len(ds["observations"]) // 1000 * 1000  # multistep: whole 1000-row episodes
+        tr = cls(spec, params, _Loader({k: v[:n_ep] for k, v in ds.items()} if cfg.model == "multistep" else ds),
+                 None, cfg)
+        tr.steps(min(20, n))
         tr.sync()
         t0 = time.perf_counter()
-        tr.steps(steps)
+        tr.steps(n)
         tr.sync()
         el = time.perf_counter() - t0
-        out[name] = {"train_steps_per_s": round(steps / el, 1), "us_per_step": round(1e6 * el / steps, 2),
+        out[name] = {"train_steps_per_s": round(n / el, 1), "us_per_step": round(1e6 * el / n, 2),
                      "final_train_loss": round(tr.read_logs()["loss"], 6)}
         tr.close()
     out["note"] = ("B=256, hidden (128, 256, 128), Adam + cosine decay; two launches per train_step "
-                   "(fused fwd/loss/bwd over 16-row blocks, partial-sum Adam)")
+                   "(fused fwd/loss/bwd over 16-row blocks, partial-sum Adam); multistep: 256-step "
+                   "windows of 1000-row episodes, backpropagation through time in one launch")
     return out
 
 

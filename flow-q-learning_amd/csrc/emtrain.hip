@@ -66,8 +66,11 @@ struct StepArgs {
     long long step;                     // update count (sampling counter)
     int B, D, A;
     float tw, ttw, alpha, gamma, rate;
-    // LDS carve-up (floats)
-    int lds_floats;
+    // multistep (FQLPOP_EM_MULTISTEP): sequence length, rows per dataset episode, and the
+    // per-(block, step) activation store of the backpropagation through time
+    int T, ep_len;
+    float* seq;
+    long long seq_stride;
 };
 
 // ----------------------------------------------------------------- Philox
@@ -158,7 +161,9 @@ DEV void dense_dx(const float* W, const float* g, int K, int N, float* g_in, con
 
 // Partial parameter grads of one Dense over the block's rows:
 // dW[k][f] = sum_r in[k][r] g[f][r], db[f] = sum_r g[f][r]
-DEV void dense_dw(const float* in, const float* g, int K, int N, float* __restrict__ pW, float* __restrict__ pb) {
+// (acc: added to the partials already there -- the sum over the steps of a sequence)
+DEV void dense_dw(const float* in, const float* g, int K, int N, float* __restrict__ pW, float* __restrict__ pb,
+                  bool acc = false) {
     for (int t = threadIdx.x; t < K * N; t += NT) {
         const int k = t / N, f = t % N;
         const float* a = in + k * R;
@@ -166,15 +171,49 @@ DEV void dense_dw(const float* in, const float* g, int K, int N, float* __restri
         float s = 0.f;
 #pragma unroll
         for (int r = 0; r < R; ++r) s = fmaf(a[r], b[r], s);
-        pW[t] = s;
+        pW[t] = acc ? pW[t] + s : s;
     }
     for (int f = threadIdx.x; f < N; f += NT) {
         const float* b = g + f * R;
         float s = 0.f;
 #pragma unroll
         for (int r = 0; r < R; ++r) s += b[r];
-        pb[f] = s;
+        pb[f] = acc ? pb[f] + s : s;
     }
+}
+
+// Frozen termination predictor on pred = tacts[0] [D][R]: weighted BCE of its logit
+// (envmodel/loss.py:14-30) into the log sums 1..5, and its input gradient, scaled by
+// tw / norm, added to gA [D][R].  inv_n: 1 / (number of scored predictions).
+DEV void tp_score(const StepArgs& a, float* const* tacts, float* gA, float* gB, float* gC, const float* lab,
+                  float (*lsum)[R], float inv_n, float norm) {
+    const Net& T = a.tpn;
+    const int tid = threadIdx.x;
+    for (int i = 0; i < T.n; ++i)
+        dense_fwd(a.tp + T.w[i], a.tp + T.b[i], tacts[i], T.dims[i], T.dims[i + 1], tacts[i + 1], i < T.n - 1);
+    if (tid < R) {
+        const float x = tacts[T.n][tid], z = lab[tid], w = a.ttw;
+        const float ce = softplus(x) - x * z;
+        lsum[1][tid] += (z > 0.f ? w * ce : ce) / (w + 1.f);
+        lsum[2][tid] += z > 0.f ? ce : 0.f;
+        lsum[3][tid] += z > 0.f ? 0.f : ce;
+        lsum[4][tid] += z;
+        lsum[5][tid] += 1.f - z;
+        const float p = 1.0f / (1.0f + expf(-x));
+        gB[tid] = (z > 0.f ? w : 1.f) / (w + 1.f) * (p - z) * inv_n;  // d bce / d logit
+    }
+    __syncthreads();
+    // dX down the frozen stack (relu' of each hidden input), gB <-> gC
+    float* src = gB;
+    float* dst = gC;
+    for (int i = T.n - 1; i >= 0; --i) {
+        dense_dx(a.tp + T.w[i], src, T.dims[i], T.dims[i + 1], dst, i > 0 ? tacts[i] : nullptr);
+        float* tmp = src;
+        src = dst;
+        dst = tmp;
+    }
+    for (int t = tid; t < a.D * R; t += NT) gA[t] += a.tw / norm * src[t];
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(NT) void em_grad_kernel(const StepArgs a) {
@@ -290,36 +329,7 @@ __global__ __launch_bounds__(NT) void em_grad_kernel(const StepArgs a) {
             atomicAdd(&lsum[0][t % R], d * d);
         }
         __syncthreads();
-        if (a.tw > 0.f) {
-            // frozen termination predictor on pred; weighted BCE (envmodel/loss.py:14-30)
-            const Net& T = a.tpn;
-            for (int i = 0; i < T.n; ++i)
-                dense_fwd(a.tp + T.w[i], a.tp + T.b[i], tacts[i], T.dims[i], T.dims[i + 1], tacts[i + 1],
-                          i < T.n - 1);
-            if (tid < R) {
-                const float x = tacts[T.n][tid], z = lab[tid], w = a.ttw;
-                const float ce = softplus(x) - x * z;
-                lsum[1][tid] = (z > 0.f ? w * ce : ce) / (w + 1.f);
-                lsum[2][tid] = z > 0.f ? ce : 0.f;
-                lsum[3][tid] = z > 0.f ? 0.f : ce;
-                lsum[4][tid] = z;
-                lsum[5][tid] = 1.f - z;
-                const float p = 1.0f / (1.0f + expf(-x));
-                gB[tid] = (z > 0.f ? w : 1.f) / (w + 1.f) * (p - z) * invB;  // d bce / d logit
-            }
-            __syncthreads();
-            // dX down the frozen stack (relu' of each hidden input), gB <-> gC
-            float* src = gB;
-            float* dst = gC;
-            for (int i = T.n - 1; i >= 0; --i) {
-                dense_dx(a.tp + T.w[i], src, T.dims[i], T.dims[i + 1], dst, i > 0 ? tacts[i] : nullptr);
-                float* tmp = src;
-                src = dst;
-                dst = tmp;
-            }
-            for (int t = tid; t < D * R; t += NT) gA[t] += a.tw / norm * src[t];
-            __syncthreads();
-        }
+        if (a.tw > 0.f) tp_score(a, tacts, gA, gB, gC, lab, lsum, invB, norm);
     } else {
         // focal loss (alpha, gamma) on the logit
         if (tid < R) {
@@ -377,6 +387,188 @@ __global__ __launch_bounds__(NT) void em_grad_kernel(const StepArgs a) {
             pg[N.ln_scale + k] = ss;
             pg[N.ln_bias + k] = sb;
         }
+    }
+}
+
+// Multistep state predictor (envmodel/multistep.py:31-54): block = 16 sequences, the
+// baseline cell stepped T times from observations[:, 0] (each step's prediction is the
+// next step's observation), the loss of every step as in em_grad_kernel (normalised over
+// B x T), then backpropagation through time: the step's activations go to a per-block
+// store in HBM on the way forward and come back in reverse; the gradient w.r.t. the
+// carried observation (the residual plus the LayerNorm input gradient of its D
+// features) flows from step t + 1 into step t.  Partial grads accumulate over the steps.
+__global__ __launch_bounds__(NT) void em_seq_grad_kernel(const StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ float lsum[NLOG][R];
+    __shared__ float lab[R];
+    __shared__ long long rowbase[R];
+    __shared__ float mu_s[R], rs_s[R], cs[2][R];
+    const int tid = threadIdx.x, blk = blockIdx.x;
+    const Net& N = a.net;
+    const int D = a.D, A = a.A, T = a.T;
+    const int K0 = N.dims[0];
+    int maxd = 0;
+    for (int i = 0; i <= N.n; ++i) maxd = max(maxd, N.dims[i]);
+    for (int i = 0; i <= a.tpn.n; ++i) maxd = max(maxd, a.tpn.dims[i]);
+    // LDS as em_grad_kernel, + carry [D][R] (the gradient w.r.t. the carried observation)
+    float* x0 = lds;
+    float* xhat = x0 + K0 * R;
+    float* acts[MAXL + 1];
+    acts[0] = xhat + K0 * R;
+    for (int i = 1; i <= N.n; ++i) acts[i] = acts[i - 1] + N.dims[i - 1] * R;
+    float* gA = acts[N.n] + N.dims[N.n] * R;
+    float* gB = gA + maxd * R;
+    float* gC = gB + maxd * R;
+    float* nobs = gC + maxd * R;
+    float* tacts[MAXL + 1];
+    tacts[0] = nobs + D * R;
+    for (int i = 1; i <= a.tpn.n; ++i) tacts[i] = tacts[i - 1] + a.tpn.dims[i - 1] * R;
+    float* carry = tacts[a.tpn.n > 0 ? a.tpn.n : 0] + (a.tpn.n > 0 ? a.tpn.dims[a.tpn.n] * R : D * R);
+
+    // ---- sequences: injected [B][T] rows, or MultistepLoader windows drawn by Philox
+    if (tid < R) {
+        const int gr = blk * R + tid;
+        long long base = (long long)gr * T;
+        if (!a.injected) {
+            uint32_t c[4] = {(uint32_t)gr, (uint32_t)a.step, 0xE5u, 0u};
+            philox(c, (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+            const long long n_ep = a.n_rows / a.ep_len;
+            const long long ep = (long long)((((uint64_t)c[1] << 32) | c[0]) % (uint64_t)n_ep);
+            const long long st = (long long)(c[2] % (uint32_t)(a.ep_len - T));
+            base = ep * a.ep_len + st;
+        }
+        rowbase[tid] = base;
+    }
+    for (int q = tid; q < NLOG * R; q += NT) lsum[q / R][q % R] = 0.f;
+    __syncthreads();
+
+    const float* P = a.params;
+    const float norm = 1.0f + a.tw;
+    const float inv_n = 1.0f / ((float)a.B * (float)T);
+    const float gscale = 2.0f / ((float)a.B * (float)T * D) / norm;
+    float* const sq = a.seq + (long long)blk * T * a.seq_stride;  // this block's store
+    // store layout per step: xhat [K0][R] | rstd [R] | acts[0..n-1] | direct output grad [D][R]
+    int act_floats = 0;
+    for (int i = 0; i < N.n; ++i) act_floats += N.dims[i] * R;
+
+    // ---- forward through the sequence
+    for (int t = 0; t < T; ++t) {
+        for (int q = tid; q < K0 * R; q += NT) {
+            const int k = q / R, r = q % R;
+            const long long row = rowbase[r] + t;
+            if (k >= D) x0[q] = a.act[row * A + (k - D)];
+            else if (t == 0) x0[q] = a.obs[row * D + k];  // later steps: the previous prediction
+        }
+        for (int q = tid; q < D * R; q += NT) {
+            const int k = q / R, r = q % R;
+            nobs[q] = a.nobs[(rowbase[r] + t) * D + k];
+        }
+        if (tid < R) lab[tid] = a.rew[rowbase[tid] + t] == 0.f ? 1.f : 0.f;
+        __syncthreads();
+        if (tid < R) {
+            float s1 = 0.f, s2 = 0.f;
+            for (int k = 0; k < K0; ++k) {
+                const float v = x0[k * R + tid];
+                s1 += v;
+                s2 += v * v;
+            }
+            const float mu = s1 / K0;
+            mu_s[tid] = mu;
+            rs_s[tid] = 1.0f / sqrtf(fmaxf(s2 / K0 - mu * mu, 0.f) + 1e-6f);
+        }
+        __syncthreads();
+        for (int q = tid; q < K0 * R; q += NT) {
+            const int k = q / R, r = q % R;
+            const float xh = (x0[q] - mu_s[r]) * rs_s[r];
+            xhat[q] = xh;
+            acts[0][q] = xh * P[N.ln_scale + k] + P[N.ln_bias + k];
+        }
+        __syncthreads();
+        for (int i = 0; i < N.n; ++i)
+            dense_fwd(P + N.w[i], P + N.b[i], acts[i], N.dims[i], N.dims[i + 1], acts[i + 1], i < N.n - 1);
+        const float* out = acts[N.n];
+        float* pred = tacts[0];
+        for (int q = tid; q < D * R; q += NT) {
+            const float p = out[q] + x0[q];
+            const float d = p - nobs[q];
+            pred[q] = p;
+            gA[q] = gscale * d;
+            atomicAdd(&lsum[0][q % R], d * d);
+        }
+        __syncthreads();
+        if (a.tw > 0.f) tp_score(a, tacts, gA, gB, gC, lab, lsum, inv_n, norm);
+        if (a.train) {
+            float* st = sq + (long long)t * a.seq_stride;
+            for (int q = tid; q < K0 * R; q += NT) st[q] = xhat[q];
+            if (tid < R) st[K0 * R + tid] = rs_s[tid];
+            float* sa = st + K0 * R + R;
+            for (int q = tid; q < act_floats; q += NT) sa[q] = acts[0][q];  // acts[0..n-1] are contiguous
+            float* sg = sa + act_floats;
+            for (int q = tid; q < D * R; q += NT) sg[q] = gA[q];
+        }
+        for (int q = tid; q < D * R; q += NT) x0[q] = pred[q];  // the next step's observation
+        __syncthreads();
+    }
+    if (tid < NLOG) {
+        float s = 0.f;
+        for (int r = 0; r < R; ++r) s += lsum[tid][r];
+        a.logs[(long long)blk * NLOG + tid] = s;
+    }
+    if (!a.train) return;
+
+    // ---- backward through time
+    float* pg = a.part + (long long)blk * a.P;
+    for (int t = T - 1; t >= 0; --t) {
+        const bool acc = t < T - 1;
+        const float* st = sq + (long long)t * a.seq_stride;
+        for (int q = tid; q < K0 * R; q += NT) xhat[q] = st[q];
+        if (tid < R) rs_s[tid] = st[K0 * R + tid];
+        const float* sa = st + K0 * R + R;
+        for (int q = tid; q < act_floats; q += NT) acts[0][q] = sa[q];
+        const float* sg = sa + act_floats;
+        // total gradient w.r.t. this step's prediction: its own loss terms + the next step's
+        for (int q = tid; q < D * R; q += NT) {
+            const float gv = sg[q] + (acc ? carry[q] : 0.f);
+            gA[q] = gv;
+            carry[q] = gv;  // the residual path: pred_t = out_t + obs_t
+        }
+        __syncthreads();
+        float* g = gA;
+        float* gn = gB;
+        for (int i = N.n - 1; i >= 0; --i) {
+            dense_dw(acts[i], g, N.dims[i], N.dims[i + 1], pg + N.w[i], pg + N.b[i], acc);
+            dense_dx(P + N.w[i], g, N.dims[i], N.dims[i + 1], gn, i > 0 ? acts[i] : nullptr);
+            float* tmp = g;
+            g = gn;
+            gn = tmp;
+        }
+        // g = grad w.r.t. the LayerNorm output [K0][R]
+        for (int k = tid; k < K0; k += NT) {
+            float ss = 0.f, sb = 0.f;
+            for (int r = 0; r < R; ++r) {
+                ss += g[k * R + r] * xhat[k * R + r];
+                sb += g[k * R + r];
+            }
+            pg[N.ln_scale + k] = acc ? pg[N.ln_scale + k] + ss : ss;
+            pg[N.ln_bias + k] = acc ? pg[N.ln_bias + k] + sb : sb;
+        }
+        if (tid < R) {
+            float c1 = 0.f, c2 = 0.f;
+            for (int k = 0; k < K0; ++k) {
+                const float gy = g[k * R + tid] * P[N.ln_scale + k];
+                c1 += gy;
+                c2 += gy * xhat[k * R + tid];
+            }
+            cs[0][tid] = c1 / K0;
+            cs[1][tid] = c2 / K0;
+        }
+        __syncthreads();
+        // LayerNorm input gradient of the observation features: into the carry
+        for (int q = tid; q < D * R; q += NT) {
+            const int k = q / R, r = q % R;
+            carry[q] += rs_s[r] * (g[q] * P[N.ln_scale + k] - cs[0][r] - xhat[q] * cs[1][r]);
+        }
+        __syncthreads();
     }
 }
 
@@ -476,13 +668,16 @@ struct fqlpop_emtrain {
     long long count = 0;
     int blocks = 0;
     int lds_bytes = 0;
+    int T = 1;                   // rows per sequence of a batch (FQLPOP_EM_MULTISTEP: sequence_length)
+    float* seq = nullptr;        // multistep: per-(block, step) activation store
+    long long seq_stride = 0;
     hipStream_t s = nullptr;
 };
 
 static void em_free(fqlpop_emtrain* h) {
     for (void* p : {(void*)h->params, (void*)h->m, (void*)h->v, (void*)h->part, (void*)h->logs, (void*)h->tp,
                     (void*)h->d_obs, (void*)h->d_act, (void*)h->d_rew, (void*)h->d_nobs, (void*)h->i_obs,
-                    (void*)h->i_act, (void*)h->i_rew, (void*)h->i_nobs, (void*)h->i_keep})
+                    (void*)h->i_act, (void*)h->i_rew, (void*)h->i_nobs, (void*)h->i_keep, (void*)h->seq})
         if (p) (void)hipFree(p);
     if (h->s) (void)hipStreamDestroy(h->s);
 }
@@ -491,7 +686,7 @@ static void em_layouts(const fqlpop_emtrain_config* c, Net* net, long long* P, N
     EMARG(c->obs_dim > 0 && c->action_dim >= 0, "bad obs/action dims");
     EMARG(c->num_hidden >= 0 && c->num_hidden < MAXL, "bad num_hidden");
     for (int i = 0; i < c->num_hidden; ++i) EMARG(c->hidden_dims[i] > 0 && c->hidden_dims[i] <= 1024, "bad hidden dim");
-    if (c->kind == FQLPOP_EM_STATE_PREDICTOR) {
+    if (c->kind == FQLPOP_EM_STATE_PREDICTOR || c->kind == FQLPOP_EM_MULTISTEP) {
         *net = layout(c->obs_dim + c->action_dim, c->num_hidden, c->hidden_dims, c->obs_dim, true, P);
         *PT = 0;
         if (c->termination_weight > 0.f) {
@@ -502,7 +697,8 @@ static void em_layouts(const fqlpop_emtrain_config* c, Net* net, long long* P, N
             tpn->ln_scale = tpn->ln_bias = -1;
         }
     } else {
-        EMARG(c->kind == FQLPOP_EM_TERMINATION, "kind must be FQLPOP_EM_STATE_PREDICTOR or FQLPOP_EM_TERMINATION");
+        EMARG(c->kind == FQLPOP_EM_TERMINATION,
+              "kind must be FQLPOP_EM_STATE_PREDICTOR, FQLPOP_EM_TERMINATION or FQLPOP_EM_MULTISTEP");
         *net = layout(c->obs_dim, c->num_hidden, c->hidden_dims, 1, false, P);
         *tpn = Net{};
         tpn->ln_scale = tpn->ln_bias = -1;
@@ -538,7 +734,16 @@ int fqlpop_emtrain_create(const fqlpop_emtrain_config* cfg, const float* params,
         int maxd = 0, sum = 0, tsum = 0;
         for (int i = 0; i <= h->net.n; ++i) { maxd = std::max(maxd, h->net.dims[i]); sum += h->net.dims[i]; }
         for (int i = 0; i <= h->tpn.n && h->tpn.n > 0; ++i) { maxd = std::max(maxd, h->tpn.dims[i]); tsum += h->tpn.dims[i]; }
-        const long long fl = (long long)R * (2 * h->net.dims[0] + sum + 3 * maxd + cfg->obs_dim + tsum);
+        const bool ms = cfg->kind == FQLPOP_EM_MULTISTEP;
+        if (ms) {
+            EMARG(cfg->sequence_length >= 1, "sequence_length must be >= 1");
+            EMARG(cfg->episode_length > cfg->sequence_length, "episode_length must exceed sequence_length");
+            h->T = cfg->sequence_length;
+        }
+        // multistep: + the carried-gradient buffer, + the prediction buffer when no frozen
+        // termination predictor owns one
+        const long long fl = (long long)R * (2 * h->net.dims[0] + sum + 3 * maxd + cfg->obs_dim + tsum +
+                                             (ms ? cfg->obs_dim * (h->tpn.n > 0 ? 1 : 2) : 0));
         EMARG(fl * 4 <= 150 * 1024, "env-model layer widths exceed the LDS budget of the fused step");
         h->lds_bytes = (int)(fl * 4);
         h->blocks = cfg->batch_size / R;
@@ -553,13 +758,21 @@ int fqlpop_emtrain_create(const fqlpop_emtrain_config* cfg, const float* params,
         EMCHK(hipMemset(h->m, 0, 4 * P));
         EMCHK(hipMemset(h->v, 0, 4 * P));
         EMCHK(hipMemset(h->logs, 0, 4 * (long long)NLOG * h->blocks));
-        const long long B = cfg->batch_size, D = cfg->obs_dim, A = cfg->action_dim;
+        const long long B = cfg->batch_size * (long long)h->T, D = cfg->obs_dim, A = cfg->action_dim;
+        if (ms) {
+            long long act = 0;
+            for (int i = 0; i < h->net.n; ++i) act += h->net.dims[i];
+            h->seq_stride = (long long)R * (h->net.dims[0] + 1 + act + D);
+            EMCHK(hipMalloc(&h->seq, 4 * h->seq_stride * h->T * h->blocks));
+        }
         EMCHK(hipMalloc(&h->i_obs, 4 * B * D));
         EMCHK(hipMalloc(&h->i_act, 4 * std::max(1LL, B * A)));
         EMCHK(hipMalloc(&h->i_rew, 4 * B));
         EMCHK(hipMalloc(&h->i_nobs, 4 * B * D));
         EMCHK(hipMalloc(&h->i_keep, B * D));
         EMCHK(hipFuncSetAttribute((const void*)em_grad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
+        EMCHK(hipFuncSetAttribute((const void*)em_seq_grad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  h->lds_bytes));
         *out = h.release();
     });
 }
@@ -590,6 +803,8 @@ int fqlpop_emtrain_set_dataset(fqlpop_emtrain_t* h, const float* obs, const floa
     return em_guard([&] {
         EMARG(h && obs && rew && next_obs && (act || h->cfg.action_dim == 0), "null argument");
         EMARG(n_rows > 0, "n_rows must be > 0");
+        if (h->cfg.kind == FQLPOP_EM_MULTISTEP)  // MultistepLoader reshapes to [n / episode_length][episode_length]
+            EMARG(n_rows % h->cfg.episode_length == 0, "multistep: n_rows must be a multiple of episode_length");
         EMCHK(hipSetDevice(h->device));
         for (float* p : {h->d_obs, h->d_act, h->d_rew, h->d_nobs})
             if (p) EMCHK(hipFree(p));
@@ -621,7 +836,7 @@ static StepArgs em_args(fqlpop_emtrain* h, bool train, bool injected) {
     a.injected = injected ? 1 : 0;
     if (injected) {
         a.obs = h->i_obs; a.act = h->i_act; a.rew = h->i_rew; a.nobs = h->i_nobs;
-        a.n_rows = c.batch_size;
+        a.n_rows = (long long)c.batch_size * h->T;
     } else {
         a.obs = h->d_obs; a.act = h->d_act; a.rew = h->d_rew; a.nobs = h->d_nobs;
         a.n_rows = h->n_rows;
@@ -629,14 +844,21 @@ static StepArgs em_args(fqlpop_emtrain* h, bool train, bool injected) {
     a.seed = c.seed;
     a.step = h->count;
     a.B = c.batch_size; a.D = c.obs_dim; a.A = c.action_dim;
-    a.tw = c.kind == FQLPOP_EM_STATE_PREDICTOR ? c.termination_weight : 0.f;
+    a.tw = c.kind != FQLPOP_EM_TERMINATION ? c.termination_weight : 0.f;
+    a.T = h->T;
+    a.ep_len = c.episode_length;
+    a.seq = h->seq;
+    a.seq_stride = h->seq_stride;
     a.ttw = c.true_termination_weight;
     a.alpha = c.focal_alpha; a.gamma = c.focal_gamma; a.rate = c.dropout_rate;
     return a;
 }
 
 static void em_launch_step(fqlpop_emtrain* h, const StepArgs& a) {
-    hipLaunchKernelGGL(em_grad_kernel, dim3(h->blocks), dim3(NT), h->lds_bytes, h->s, a);
+    if (h->cfg.kind == FQLPOP_EM_MULTISTEP)
+        hipLaunchKernelGGL(em_seq_grad_kernel, dim3(h->blocks), dim3(NT), h->lds_bytes, h->s, a);
+    else
+        hipLaunchKernelGGL(em_grad_kernel, dim3(h->blocks), dim3(NT), h->lds_bytes, h->s, a);
     EMCHK(hipGetLastError());
     if (!a.train) return;
     // optax.cosine_decay_schedule(init, steps)(count), adam bias correction with count + 1
@@ -654,7 +876,7 @@ static void em_launch_step(fqlpop_emtrain* h, const StepArgs& a) {
 }
 
 static void em_check_ready(fqlpop_emtrain* h) {
-    if (h->cfg.kind == FQLPOP_EM_STATE_PREDICTOR && h->cfg.termination_weight > 0.f && !h->tp)
+    if (h->cfg.kind != FQLPOP_EM_TERMINATION && h->cfg.termination_weight > 0.f && !h->tp)
         throw EmErr{FQLPOP_E_STATE, "termination_weight > 0 needs fqlpop_emtrain_set_frozen_termination"};
 }
 
@@ -671,7 +893,7 @@ int fqlpop_emtrain_step(fqlpop_emtrain_t* h, int n_steps) {
 static void em_upload_batch(fqlpop_emtrain* h, const float* obs, const float* act, const float* rew,
                             const float* next_obs) {
     EMARG(obs && rew && next_obs && (act || h->cfg.action_dim == 0), "null batch array");
-    const long long B = h->cfg.batch_size, D = h->cfg.obs_dim, A = h->cfg.action_dim;
+    const long long B = (long long)h->cfg.batch_size * h->T, D = h->cfg.obs_dim, A = h->cfg.action_dim;
     EMCHK(hipMemcpyAsync(h->i_obs, obs, 4 * B * D, hipMemcpyHostToDevice, h->s));
     if (A) EMCHK(hipMemcpyAsync(h->i_act, act, 4 * B * A, hipMemcpyHostToDevice, h->s));
     EMCHK(hipMemcpyAsync(h->i_rew, rew, 4 * B, hipMemcpyHostToDevice, h->s));
@@ -704,9 +926,9 @@ static void em_logs(fqlpop_emtrain* h, float* out) {
     double s[NLOG] = {0};
     for (int b = 0; b < h->blocks; ++b)
         for (int k = 0; k < NLOG; ++k) s[k] += lg[(size_t)b * NLOG + k];
-    const double B = h->cfg.batch_size, D = h->cfg.obs_dim;
+    const double B = (double)h->cfg.batch_size * h->T, D = h->cfg.obs_dim;  // scored predictions
     for (int k = 0; k < FQLPOP_EM_LOG_STRIDE; ++k) out[k] = 0.f;
-    if (h->cfg.kind == FQLPOP_EM_STATE_PREDICTOR) {
+    if (h->cfg.kind != FQLPOP_EM_TERMINATION) {
         const double mse = s[0] / (B * D), tw = h->cfg.termination_weight;
         const double tl = tw > 0 ? s[1] / B : 0.0;
         out[0] = (float)((mse + tw * tl) / (1.0 + tw));

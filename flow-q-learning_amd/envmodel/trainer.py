@@ -35,6 +35,7 @@ SP_LOG_KEYS = ("loss", "next_observation_loss", "termination_loss", "true_termin
                "false_termination_loss")
 TP_TRAIN_LOG_KEYS = ("loss", "true_loss", "false_loss")
 TP_EVAL_LOG_KEYS = ("loss", "true_loss", "false_loss", "accuracy", "precision", "recall")
+MULTISTEP_EPISODE_LENGTH = 1000  # utils/data_loader.py:30 reshapes the dataset into 1000-step episodes
 
 
 @dataclass
@@ -86,12 +87,17 @@ class _GpuEnvModelTrainer:
     def __init__(self, spec: em.EnvModelSpec, params: dict, train_loader, val_loader, config: EnvModelTrainerConfig,
                  logger=None, device: int = 0, tp_params: dict | None = None, focal_alpha=DEFAULT_FOCAL_ALPHA,
                  focal_gamma=DEFAULT_FOCAL_GAMMA, dropout_rate=DEFAULT_DROPOUT):
-        from fqlpop._lib import EmTrainConfig, check, fptr, load_library
+        from fqlpop._lib import EM_MULTISTEP, EmTrainConfig, check, fptr, load_library
         self._lib, self._check, self._fptr = load_library(), check, fptr
         self.spec, self.config, self.logger = spec, config, logger
         self.train_loader, self.val_loader = train_loader, val_loader
+        # the multistep model (train_env_model.py:46-66) trains the same cell through a scan
+        self._ms = self.kind == 0 and getattr(config, "model", "baseline") == "multistep"
+        self._T = int(config.sequence_length) if self._ms else 1
         c = EmTrainConfig()
-        c.kind = self.kind
+        c.kind = EM_MULTISTEP if self._ms else self.kind
+        c.sequence_length = self._T
+        c.episode_length = int(getattr(train_loader, "episode_length", MULTISTEP_EPISODE_LENGTH)) if self._ms else 0
         c.obs_dim, c.action_dim = spec.obs_dim, spec.action_dim
         hid = spec.sp_hidden if self.kind == 0 else spec.tp_hidden
         c.num_hidden = len(hid)
@@ -136,16 +142,23 @@ class _GpuEnvModelTrainer:
 
     # ------------------------------------------------------------- plumbing
     def _set_dataset(self, ds: dict):
-        arrs = [_f32(ds["observations"]), _f32(ds.get("actions", np.zeros((len(ds["observations"]), 0)))),
-                _f32(ds["rewards"]), _f32(ds["next_observations"])]
+        # rows (a multistep loader holds [episodes][episode_length][..]: flattened back to rows)
+        D, A = self.spec.obs_dim, self.spec.action_dim
+        obs = _f32(ds["observations"]).reshape(-1, D)
+        act = _f32(ds["actions"]).reshape(-1, A) if "actions" in ds else np.zeros((len(obs), A), np.float32)
+        arrs = [obs, np.ascontiguousarray(act), _f32(ds["rewards"]).reshape(-1),
+                _f32(ds["next_observations"]).reshape(-1, D)]
         self._check(self._lib.fqlpop_emtrain_set_dataset(self._h, *[self._fptr(a) for a in arrs], len(arrs[0])))
 
     def _batch_ptrs(self, batch: dict):
         B = self.config.batch_size
-        arrs = [_f32(batch["observations"]), _f32(batch.get("actions", np.zeros((B, self.spec.action_dim)))),
+        arrs = [_f32(batch["observations"]),
+                _f32(batch.get("actions", np.zeros(np.shape(batch["observations"])[:-1] + (self.spec.action_dim,)))),
                 _f32(batch["rewards"]), _f32(batch["next_observations"])]
         if arrs[0].shape[0] != B:
             raise ValueError(f"batch has {arrs[0].shape[0]} rows, batch_size is {B}")
+        if self._ms and (arrs[0].ndim != 3 or arrs[0].shape[1] != self._T):
+            raise ValueError(f"multistep batches are [B, {self._T}, ..], got {arrs[0].shape}")
         return arrs
 
     def _logs(self, v: np.ndarray, keys) -> dict:
@@ -179,6 +192,11 @@ class _GpuEnvModelTrainer:
         out = np.zeros(8, np.float32)
         self._check(self._lib.fqlpop_emtrain_read_logs(self._h, self._fptr(out)))
         return self._logs(out, self._train_keys())
+
+    def learning_rate(self, step: int) -> float:
+        """optax.cosine_decay_schedule(init_learning_rate, steps)(step)."""
+        c = min(step, self.config.steps)
+        return self.config.init_learning_rate * 0.5 * (1.0 + np.cos(np.pi * c / self.config.steps))
 
     def sync(self):
         self._check(self._lib.fqlpop_emtrain_sync(self._h))
@@ -215,12 +233,12 @@ class _GpuEnvModelTrainer:
                 self._val(step)
             if self._device_sampling:
                 self.steps(1)
-                if self.logger:
-                    self.logger.log({f"train/{k}": v for k, v in self.read_logs().items()}, step=step)
+                logs = self.read_logs() if self.logger else None
             else:
                 _, logs = self.train_step(None, self.train_loader.sample(self.config.batch_size))
-                if self.logger:
-                    self.logger.log({f"train/{k}": v for k, v in logs.items()}, step=step)
+            if self.logger:
+                self.logger.log({"train/learning_rate": self.learning_rate(step),
+                                 **{f"train/{k}": v for k, v in logs.items()}}, step=step)
         self._val(self.config.steps)
 
     def close(self):
@@ -236,7 +254,9 @@ class _GpuEnvModelTrainer:
 
 
 class StatePredictorTrainer(_GpuEnvModelTrainer):
-    """envmodel/state_predictor_trainer.py:22-170 (baseline model)."""
+    """envmodel/state_predictor_trainer.py:22-170: the baseline model, or the multistep
+    model (envmodel/multistep.py) when ``config.model == "multistep"`` -- then batches
+    are [B, sequence_length, ..] windows and ``params`` is the scanned cell's tree."""
     kind = 0
 
     def _train_keys(self):

@@ -68,10 +68,11 @@ class EmTrainConfig(ctypes.Structure):
         ("focal_gamma", ctypes.c_float), ("dropout_rate", ctypes.c_float),
         ("seed", ctypes.c_uint64),
         ("tp_num_hidden", ctypes.c_int), ("tp_hidden_dims", ctypes.c_int * 8),
+        ("sequence_length", ctypes.c_int), ("episode_length", ctypes.c_int),
     ]
 
 
-EM_STATE_PREDICTOR, EM_TERMINATION = 0, 1
+EM_STATE_PREDICTOR, EM_TERMINATION, EM_MULTISTEP = 0, 1, 2
 EM_LOG_STRIDE = 8
 _P = ctypes.c_void_p
 _F = ctypes.POINTER(ctypes.c_float)

@@ -5,8 +5,9 @@ OGBench-style .npz dataset (ogbench / wandb are absent: data must already be in
 
 Saves ``<save_directory>/<env_name>/env_models/<model>.pt`` (flax
 ``to_bytes`` of the params tree, readable by utils/envmodel.py:load_model) and
-``<model>_config.yaml``, as train_env_model.py:127-137 does.  The
-``multistep`` model (BPTT through a 256-step scan) is not built: it raises.
+``<model>_config.yaml``, as train_env_model.py:127-137 does.  ``multistep`` trains
+the baseline cell through a ``--sequence_length`` scan (BPTT on the GPU) and saves
+it under ``params/ScanCell_0/cell`` like flax's ``nn.scan`` tree.
 """
 from __future__ import annotations
 
@@ -40,6 +41,29 @@ class StepLoader:
         return {k: v[idx] for k, v in self.dataset.items()}
 
 
+class MultistepLoader:
+    """utils/data_loader.py:25-39: the dataset as [n / 1000][1000] episodes; a batch is
+    batch_size windows of sequence_length steps (uniform episode, uniform start in
+    [0, 1000 - sequence_length))."""
+
+    episode_length = 1000
+
+    def __init__(self, dataset: dict, sequence_length: int = 128):
+        self.sequence_length = sequence_length
+        n = len(dataset["observations"])
+        if n % self.episode_length:
+            raise ValueError(f"multistep: {n} rows is not a whole number of {self.episode_length}-step episodes")
+        shape = (n // self.episode_length, self.episode_length)
+        self.dataset = {k: np.asarray(dataset[k]).reshape(shape + np.shape(dataset[k])[1:])
+                        for k in ("observations", "actions", "rewards", "next_observations")}
+
+    def sample(self, batch_size: int) -> dict:
+        ep = np.random.randint(len(self.dataset["observations"]), size=batch_size)
+        start = np.random.randint(0, self.episode_length - self.sequence_length, size=batch_size)
+        idx = start[:, None] + np.arange(self.sequence_length)
+        return {k: v[ep[:, None], idx] for k, v in self.dataset.items()}
+
+
 class _CsvRunLogger:
     """wandb.log stand-in: long-format CSV (step, key, value) -- train and val rows carry
     different keys, so a fixed-header CSV would drop some."""
@@ -65,7 +89,7 @@ def main(argv=None):
     save_dir.mkdir(parents=True, exist_ok=True)
     logger = _CsvRunLogger(save_dir / f"{config.model}_log.csv")
     np.random.seed(config.seed)
-    if config.model == "baseline":
+    if config.model in ("baseline", "multistep"):
         spec = em.EnvModelSpec(D, A, hidden, em.DEFAULT_HIDDEN)
         tp = None
         if config.termination_weight > 0:  # utils/envmodel.py load_model("termination_predictor")
@@ -73,19 +97,26 @@ def main(argv=None):
             tp = tp.get("params", tp)
             n = sum(1 for k in tp if k.startswith("Dense_"))
             spec.tp_hidden = tuple(int(np.asarray(tp[f"Dense_{i}"]["kernel"]).shape[1]) for i in range(n - 1))
-        trainer = StatePredictorTrainer(spec, em.init_state_predictor(spec, config.seed), StepLoader(train),
-                                        StepLoader(val), config, logger=logger, tp_params=tp)
+        if config.model == "multistep":
+            loaders = (MultistepLoader(train, config.sequence_length), MultistepLoader(val, config.sequence_length))
+        else:
+            loaders = (StepLoader(train), StepLoader(val))
+        trainer = StatePredictorTrainer(spec, em.init_state_predictor(spec, config.seed), *loaders, config,
+                                        logger=logger, tp_params=tp)
     elif config.model == "termination_predictor":
         spec = em.EnvModelSpec(D, A, em.DEFAULT_HIDDEN, hidden)
         trainer = TerminationPredictorTrainer(spec, em.init_termination_predictor(spec, config.seed),
                                               StepLoader(train), StepLoader(val), config, logger=logger)
     else:
-        raise ValueError(f"model {config.model!r} is not built here (baseline, termination_predictor)")
+        raise ValueError(f"unknown model {config.model!r} (baseline, multistep, termination_predictor)")
     trainer.train()
     with open(save_dir / f"{config.model}_config.yaml", "w") as f:
         yaml.safe_dump({k: list(v) if isinstance(v, tuple) else v for k, v in config.model_config.items()}, f)
     with open(save_dir / f"{config.model}.pt", "wb") as f:
-        f.write(msgpack_serialize({"params": trainer.params}))
+        params = trainer.params
+        if config.model == "multistep":  # nn.scan(Cell) tree (envmodel/multistep.py:41-52)
+            params = {"ScanCell_0": {"cell": params}}
+        f.write(msgpack_serialize({"params": params}))
     trainer.close()
     return save_dir
 

@@ -238,7 +238,14 @@ int fqlpop_envmodel_step(fqlpop_t* h, const float* obs, const float* actions, in
  *     (state_predictor_trainer.py:57-61).
  * Parameters are flat vectors in flax leaf order (path-sorted): Dense_i/bias,
  * Dense_i/kernel ([in][out]) ..., then LayerNorm_0/bias, LayerNorm_0/scale. */
-enum { FQLPOP_EM_STATE_PREDICTOR = 0, FQLPOP_EM_TERMINATION = 1 };
+enum { FQLPOP_EM_STATE_PREDICTOR = 0, FQLPOP_EM_TERMINATION = 1, FQLPOP_EM_MULTISTEP = 2 };
+/* FQLPOP_EM_MULTISTEP: the same trainer on MultistepStatePredictor
+ *   (envmodel/multistep.py:31-54, train_env_model.py:46-66): the baseline cell scanned
+ *   over sequence_length steps from observations[:, 0] (each prediction is the next
+ *   step's observation), state_prediction_loss over all B x T predictions, gradients by
+ *   backpropagation through time.  Batches are [B][T][..]; device sampling draws
+ *   MultistepLoader windows (utils/data_loader.py:25-39): a uniform episode of
+ *   episode_length rows, a uniform start in [0, episode_length - T). */
 #define FQLPOP_EM_LOG_STRIDE 8
 /* logs: state predictor  [loss, next_observation_loss, termination_loss,
  *                         true_termination_loss, false_termination_loss]
@@ -259,6 +266,8 @@ typedef struct fqlpop_emtrain_config {
     uint64_t seed;                 /* device sampling and the fixed dropout mask */
     int tp_num_hidden;             /* frozen termination predictor (termination_weight > 0) */
     int tp_hidden_dims[8];
+    int sequence_length;           /* FQLPOP_EM_MULTISTEP: T (--sequence_length, 256) */
+    int episode_length;            /* FQLPOP_EM_MULTISTEP device sampling: rows per episode (1000) */
 } fqlpop_emtrain_config;
 typedef struct fqlpop_emtrain fqlpop_emtrain_t;
 

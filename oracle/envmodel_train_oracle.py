@@ -5,6 +5,8 @@ step of the reference's world-model trainers.  Used only
 by ``tests/`` as the checker of ``fqlpop_emtrain_*`` (the product path never
 imports it):
 
+* multistep state predictor -- the same step on ``MultistepStatePredictor``
+  (envmodel/multistep.py:31-54), backpropagation through time (``multistep_step``);
 * state predictor -- ``StatePredictorTrainer.train_step``
   (envmodel/state_predictor_trainer.py:67-95) on ``BaselineStatePredictor``
   (envmodel/baseline.py:25-37) with ``state_prediction_loss``
@@ -133,6 +135,86 @@ def state_predictor_step(tree: dict, batch: dict, termination_weight: float = 0.
     grads, g_h0 = _relu_mlp_bwd(tree, ins, g_pred)
     grads["LayerNorm_0"] = {"scale": (g_h0 * xhat).sum(0), "bias": g_h0.sum(0)}
     return loss, logs, grads, pred
+
+
+def _ln_fwd(x0: np.ndarray):
+    mu = x0.mean(-1, keepdims=True)
+    var = np.maximum((x0 * x0).mean(-1, keepdims=True) - mu * mu, 0.0)
+    rs = 1.0 / np.sqrt(var + LN_EPS)
+    return (x0 - mu) * rs, rs
+
+
+def multistep_step(tree: dict, batch: dict, termination_weight: float = 0.0,
+                   true_termination_weight: float = 30.0, tp_tree: dict | None = None):
+    """Loss, logs and parameter grads of one train_step on MultistepStatePredictor
+    (envmodel/multistep.py:31-54; train_env_model.py:46-66 binding, reconstruction
+    weight 0): the baseline cell scanned over the T steps of [B, T, ..] sequences from
+    observations[:, 0] (the carry is each step's prediction), state_prediction_loss
+    (envmodel/loss.py:80-111) over all B x T predictions, gradients by
+    backpropagation through time.  Returns (loss, logs, grads, predictions [B, T, D])."""
+    obs = np.asarray(batch["observations"], np.float64)
+    act = np.asarray(batch["actions"], np.float64)
+    nxt = np.asarray(batch["next_observations"], np.float64)
+    term = (np.asarray(batch["rewards"]) == 0).astype(np.float64)
+    B, T, D = obs.shape
+    ln = tree["LayerNorm_0"]
+    scale = np.asarray(ln["scale"], np.float64)
+    bias = np.asarray(ln["bias"], np.float64)
+    tw = float(termination_weight)
+    norm = 1.0 + tw
+    w = float(true_termination_weight)
+    o = obs[:, 0]
+    caches, g_direct, preds = [], [], []
+    sq, tl_sum, fl_sum, t_loss_sum = 0.0, 0.0, 0.0, 0.0
+    for t in range(T):
+        xhat, rs = _ln_fwd(np.concatenate([o, act[:, t]], -1))
+        out, ins = _relu_mlp_fwd(tree, xhat * scale + bias)
+        pred = out + o
+        diff = pred - nxt[:, t]
+        sq += float((diff * diff).sum())
+        g = 2.0 * diff / (B * T * D)
+        if tw > 0:
+            logit, tins = _relu_mlp_fwd(tp_tree, pred)
+            logit = logit[:, 0]
+            z = term[:, t]
+            ce = sigmoid_bce(logit, z)
+            tl_sum += float(np.where(z == 1, ce, 0.0).sum())
+            fl_sum += float(np.where(z == 0, ce, 0.0).sum())
+            t_loss_sum += float(((w * np.where(z == 1, ce, 0.0) + np.where(z == 0, ce, 0.0)) / (w + 1)).sum())
+            p = 1.0 / (1.0 + np.exp(-logit))
+            g_logit = np.where(z == 1, w, 1.0) / (w + 1) * (p - z) / (B * T)
+            _, g_tp_in = _relu_mlp_bwd(tp_tree, tins, g_logit[:, None], want_params=False)
+            g = g + tw * g_tp_in
+        caches.append((xhat, rs, ins))
+        g_direct.append(g / norm)
+        preds.append(pred)
+        o = pred
+    mse = sq / (B * T * D)
+    logs = {"next_observation_loss": mse}
+    t_loss = 0.0
+    if tw > 0:
+        t_loss = t_loss_sum / (B * T)
+        n_pos, n_neg = term.sum(), (1 - term).sum()
+        logs["termination_loss"] = t_loss
+        logs["true_termination_loss"] = tl_sum / n_pos if n_pos > 0 else float("nan")
+        logs["false_termination_loss"] = fl_sum / n_neg if n_neg > 0 else float("nan")
+    loss = (mse + tw * t_loss) / norm
+    logs["loss"] = loss
+    grads = zeros_like_tree(tree)
+    carry = np.zeros((B, D))
+    for t in reversed(range(T)):
+        xhat, rs, ins = caches[t]
+        G = g_direct[t] + carry
+        gt, g_h0 = _relu_mlp_bwd(tree, ins, G)
+        for mod, d in gt.items():
+            for leaf, v in d.items():
+                grads[mod][leaf] += v
+        grads["LayerNorm_0"]["scale"] += (g_h0 * xhat).sum(0)
+        grads["LayerNorm_0"]["bias"] += g_h0.sum(0)
+        gy = g_h0 * scale
+        g_x0 = rs * (gy - gy.mean(-1, keepdims=True) - xhat * (gy * xhat).mean(-1, keepdims=True))
+        carry = G + g_x0[:, :D]  # residual + the LayerNorm input path of the carried observation
+    return loss, logs, grads, np.stack(preds, 1)
 
 
 def focal_terms(logits, labels, alpha=0.25, gamma=2.0):

@@ -14,6 +14,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "flow-q-learning_amd"))
 
 from oracle import envmodel_train_oracle as T  # noqa: E402
+T_ = T
 import envmodel as em  # noqa: E402
 
 
@@ -166,3 +167,67 @@ def test_trainer_flat_layout_roundtrip():
     for m in tp:
         for k in tp[m]:
             np.testing.assert_array_equal(tree[m][k], tp[m][k])
+
+
+def _seq_batch(rng, B, T, D, A, p_term=0.2):
+    obs = rng.standard_normal((B, T, D))
+    return {"observations": obs, "actions": rng.uniform(-1, 1, (B, T, A)),
+            "next_observations": obs + 0.1 * rng.standard_normal((B, T, D)),
+            "rewards": np.where(rng.uniform(size=(B, T)) < p_term, 0.0, -1.0)}
+
+
+@pytest.mark.parametrize("tw", [0.0, 1.0])
+def test_multistep_bptt_grads_vs_autograd(tw):
+    """oracle.multistep_step (hand-written BPTT) against torch autograd through the
+    scanned cell (envmodel/multistep.py:31-54) in float64."""
+    rng = np.random.default_rng(4)
+    B, T, D, A = 3, 6, 7, 3
+    spec = em.EnvModelSpec(D, A, (16, 24, 16), (12, 12))
+    sp = em.init_state_predictor(spec, 1)
+    sp["LayerNorm_0"]["scale"] = (1 + 0.1 * rng.standard_normal(D + A)).astype(np.float32)
+    sp["LayerNorm_0"]["bias"] = (0.1 * rng.standard_normal(D + A)).astype(np.float32)
+    tp = em.init_termination_predictor(spec, 2)
+    b = _seq_batch(rng, B, T, D, A, p_term=0.3)
+    loss, logs, grads, preds = T_.multistep_step(sp, b, tw, 30.0, tp)
+    tt = _torch_tree(sp)
+    ttp = {m: {k: torch.tensor(np.asarray(v, np.float64)) for k, v in d.items()} for m, d in tp.items()}
+    dense = {k: v for k, v in tt.items() if k.startswith("Dense_")}
+    o = torch.tensor(b["observations"][:, 0])
+    act = torch.tensor(b["actions"])
+    out = []
+    for t in range(T):
+        h0 = _ln_torch(torch.cat([o, act[:, t]], -1), tt["LayerNorm_0"]["scale"], tt["LayerNorm_0"]["bias"])
+        o = _torch_mlp(dense, h0) + o
+        out.append(o)
+    pred = torch.stack(out, 1)
+    mse = ((pred - torch.tensor(b["next_observations"])) ** 2).mean()
+    total = mse
+    if tw > 0:
+        logit = _torch_mlp(ttp, pred)[..., 0]
+        z = torch.tensor((b["rewards"] == 0).astype(np.float64))
+        ce = _bce_torch(logit, z)
+        tl = torch.where(z == 1, ce, torch.zeros_like(ce))
+        fl = torch.where(z == 0, ce, torch.zeros_like(ce))
+        total = mse + tw * ((30.0 * tl + fl) / 31.0).mean()
+        assert logs["true_termination_loss"] == pytest.approx(float(tl.detach().sum() / (z == 1).sum()), rel=1e-12)
+    total = total / (1 + tw)
+    total.backward()
+    np.testing.assert_allclose(preds, pred.detach().numpy(), rtol=1e-12, atol=1e-12)
+    assert abs(loss - total.item()) < 1e-12
+    assert abs(logs["next_observation_loss"] - mse.item()) < 1e-12
+    for m, d in tt.items():
+        for k, v in d.items():
+            np.testing.assert_allclose(grads[m][k], v.grad.numpy(), rtol=1e-9, atol=1e-12, err_msg=f"{m}/{k}")
+
+
+def test_multistep_one_step_is_the_baseline_step():
+    rng = np.random.default_rng(5)
+    spec = em.EnvModelSpec(9, 2, (8, 8))
+    sp = em.init_state_predictor(spec, 3)
+    b = _seq_batch(rng, 4, 1, 9, 2)
+    l1, _, g1, _ = T_.multistep_step(sp, b)
+    l0, _, g0, _ = T_.state_predictor_step(sp, {k: v[:, 0] for k, v in b.items()})
+    assert l1 == pytest.approx(l0, rel=1e-13)
+    for m in g0:
+        for k in g0[m]:
+            np.testing.assert_allclose(g1[m][k], g0[m][k], rtol=1e-12, atol=1e-15)

@@ -9,6 +9,8 @@ import envmodel as em
 from envmodel.trainer import EnvModelTrainerConfig, StatePredictorTrainer, TerminationPredictorTrainer
 from oracle import envmodel_train_oracle as T
 
+T_ = T
+
 pytestmark = pytest.mark.gpu
 
 
@@ -114,6 +116,44 @@ def test_termination_predictor_steps_match_oracle():
     tr.close()
 
 
+def _seq_batch(rng, B, T, D, A, p_term=0.25):
+    obs = rng.standard_normal((B, T, D)).astype(np.float32)
+    return {"observations": obs, "actions": rng.uniform(-1, 1, (B, T, A)).astype(np.float32),
+            "next_observations": (obs + 0.1 * rng.standard_normal((B, T, D))).astype(np.float32),
+            "rewards": np.where(rng.uniform(size=(B, T)) < p_term, 0.0, -1.0).astype(np.float32)}
+
+
+@pytest.mark.parametrize("tw,T", [(0.0, 8), (1.0, 8), (0.0, 48)])
+def test_multistep_steps_match_oracle(tw, T):
+    """FQLPOP_EM_MULTISTEP (BPTT through the scanned cell) against oracle.multistep_step:
+    logs, Adam moments and parameters after every injected step."""
+    D, A = 28, 5
+    spec = em.EnvModelSpec(D, A, (128, 256, 128), (128, 256, 128) if tw > 0 else (64,))
+    rng = np.random.default_rng(7)
+    sp = em.init_state_predictor(spec, 1)
+    sp["LayerNorm_0"]["scale"] = (1 + 0.1 * rng.standard_normal(D + A)).astype(np.float32)
+    sp["LayerNorm_0"]["bias"] = (0.1 * rng.standard_normal(D + A)).astype(np.float32)
+    tp = em.init_termination_predictor(spec, 2)
+    cfg = EnvModelTrainerConfig(steps=50, model="multistep", sequence_length=T, termination_weight=tw,
+                                batch_size=32, init_learning_rate=1e-3)
+    tr = StatePredictorTrainer(spec, sp, None, None, cfg, tp_params=tp if tw > 0 else None)
+    ref, m, v = _f64(sp), T_.zeros_like_tree(sp), T_.zeros_like_tree(sp)
+    for step in range(3):
+        b = _seq_batch(rng, 32, T, D, A)
+        _, logs = tr.train_step(None, b)
+        _, want_logs, grads, _ = T_.multistep_step(ref, b, tw, 30.0, _f64(tp))
+        for k in logs:
+            assert logs[k] == pytest.approx(want_logs[k], rel=2e-4, abs=1e-7), (step, k)
+        ref, m, v = T_.adam_update(ref, grads, m, v, step, T_.cosine_lr(1e-3, 50, step))
+        _assert_moments_close(tr, m)
+        _assert_params_close(tr.params, ref, step + 1)
+    logs = tr.eval_step(None, _seq_batch(rng, 32, T, D, A))
+    assert np.isfinite(logs["loss"])
+    with pytest.raises(ValueError):
+        tr.train_step(None, _batch(rng, 32, D, A))  # single-step batches are refused
+    tr.close()
+
+
 class _Loader:
     def __init__(self, ds):
         self.dataset = ds
@@ -205,5 +245,54 @@ def test_train_env_model_driver(tmp_path):
     sp = em.load_flax_msgpack(out / "baseline.pt")["params"]
     assert sp["LayerNorm_0"]["scale"].shape == (D + A,)
     assert (out / "baseline_config.yaml").exists() and (out / "baseline_log.csv").exists()
-    with pytest.raises(ValueError):
-        tem.main(["--model=multistep", "--steps=10"] + common)
+
+
+def _trajectory_dataset(n_ep, D, A, seed=0):
+    """Episode-major rows of 1000-step trajectories: o' = 0.9 o + 0.3 tanh([o, a] M)."""
+    rng = np.random.default_rng(seed)
+    M = (0.3 * rng.standard_normal((D + A, D))).astype(np.float32)
+    o = rng.standard_normal((n_ep, D)).astype(np.float32)
+    cols = {k: [] for k in ("observations", "actions", "next_observations")}
+    for _ in range(1000):
+        a = rng.uniform(-1, 1, (n_ep, A)).astype(np.float32)
+        o2 = (0.9 * o + 0.3 * np.tanh(np.concatenate([o, a], 1) @ M)).astype(np.float32)
+        cols["observations"].append(o)
+        cols["actions"].append(a)
+        cols["next_observations"].append(o2)
+        o = o2
+    ds = {k: np.stack(v, 1).reshape(n_ep * 1000, -1) for k, v in cols.items()}
+    ds["rewards"] = np.where(ds["next_observations"][:, 0] > 1.0, 0.0, -1.0).astype(np.float32)
+    return ds
+
+
+def test_multistep_device_sampling_learns_and_driver(tmp_path):
+    """Device-sampled MultistepLoader windows: deterministic for a seed, the rollout loss
+    falls; then train_env_model.py --model=multistep end to end (flax nn.scan tree)."""
+    import train_env_model as tem
+    D, A = 28, 5
+    ds = _trajectory_dataset(8, D, A, seed=11)
+    spec = em.EnvModelSpec(D, A)
+    sp = em.init_state_predictor(spec, 0)
+    cfg = EnvModelTrainerConfig(steps=150, model="multistep", sequence_length=16, termination_weight=0.0,
+                                batch_size=64, seed=3)
+    runs = []
+    for _ in range(2):
+        ld = tem.MultistepLoader(dict(ds), 16)
+        np.random.seed(0)
+        b = ld.sample(64)
+        tr = StatePredictorTrainer(spec, sp, ld, None, cfg)
+        before = tr.eval_step(None, b)["next_observation_loss"]
+        tr.steps(150)
+        after = tr.eval_step(None, b)["next_observation_loss"]
+        runs.append((before, after, tr.flat()))
+        tr.close()
+    assert runs[0][1] < 0.5 * runs[0][0], runs[0][:2]
+    np.testing.assert_array_equal(runs[0][2], runs[1][2])
+    data = tmp_path / "data"
+    data.mkdir()
+    np.savez(data / "cube-single-play.npz", **{k: ds[k][:3000] for k in ds})
+    out = tem.main(["--model=multistep", "--steps=40", "--sequence_length=16", "--termination_weight=0",
+                    f"--data_directory={data}", f"--save_directory={tmp_path / 'exp'}", "--val_batches=2"])
+    tree = em.load_flax_msgpack(out / "multistep.pt")["params"]
+    cell = tree["ScanCell_0"]["cell"]
+    assert cell["Dense_0"]["kernel"].shape == (D + A, 128) and cell["LayerNorm_0"]["scale"].shape == (D + A,)
