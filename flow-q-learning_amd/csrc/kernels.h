@@ -173,6 +173,7 @@ struct StreamArgs {
     float* RS[EF_MAX_LAYERS];             // LN 1/sigma
     long long s_ss, s_sy, st_ss, st_sy;
     int ld_s, st_lo, st_hi;
+    int g_hi;                             // G is stored for columns [st_lo, g_hi) only (<= st_hi)
     HeadArgs head;                        // head outputs (head.M/.ld unused)
     int ny, nz;
     const int* slots;

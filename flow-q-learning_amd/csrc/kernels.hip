@@ -1210,7 +1210,7 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
         __syncthreads();  // every wave is done reading the slab; lnp visible
 
         // activation stores: buffer ops, per-lane offset + wave-uniform row offset (no 64-bit address VGPRs)
-        const bool stU = st && g.U[l], stG = st && g.G[l];
+        const bool stU = st && g.U[l], stG = st && g.G[l] && c0 + NC <= g.g_hi;
         const long long sbase = (long long)slot * g.s_ss + (long long)y * g.s_sy + c0;
         const rsrc_t rU = make_rsrc(stU ? g.U[l] + sbase : g.params, stU ? (long long)H * g.ld_s : 0);
         const rsrc_t rG = make_rsrc(stG ? g.G[l] + sbase : g.params, stG ? (long long)H * g.ld_s : 0);

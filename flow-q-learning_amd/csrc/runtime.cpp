@@ -756,7 +756,7 @@ void adam_net(const Ctx& c, hipStream_t s, int ni) {
 void stream_fwd(const Ctx& c, hipStream_t s, const NetLayout& N, const float* arena, long long P, TRef X, int ldx,
                 int M, const std::vector<float*>* U, const std::vector<float*>* G, const std::vector<float*>* MU,
                 const std::vector<float*>* RS, long long s_ss, long long s_sy, long long st_ss, long long st_sy,
-                int st_lo, int st_hi, int mode, const HeadArgs& head) {
+                int st_lo, int st_hi, int mode, const HeadArgs& head, int g_hi = -1) {
     fqlpop* h = c.h;
     StreamArgs a{};
     a.params = arena + N.off;
@@ -781,6 +781,7 @@ void stream_fwd(const Ctx& c, hipStream_t s, const NetLayout& N, const float* ar
     a.ld_x = ldx; a.K0 = N.in_dim; a.L = N.L; a.M = M;
     a.s_ss = s_ss; a.s_sy = s_sy; a.st_ss = st_ss; a.st_sy = st_sy;
     a.ld_s = ldx; a.st_lo = st_lo; a.st_hi = st_hi;
+    a.g_hi = g_hi < 0 ? st_hi : g_hi;
     a.head = head;
     a.head.nout = N.out_dim;
     a.ny = N.E; a.nz = c.nz; a.slots = h->slots;
@@ -1011,9 +1012,11 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         HeadArgs hc = head_args(c, N, h->cr_h[L - 1], B2, B2, sy2);
         hc.o0 = tref(h->q, (long long)E * B2, B2); hc.ld0 = B2;
         if (h->stream_fwd) {
+            // the a_pi columns [B, 2B) are back-propagated for dQ/da only: their layer outputs
+            // (the dW GEMMs' operand) are not needed by the streamed backward
             stream_fwd(c, sM, N, h->params, h->P, tref(h->cr_in, (long long)Kc * B2, 0), B2, B2, &h->cr_u, &h->cr_h,
                        N.ln ? &h->cr_mu : nullptr, N.ln ? &h->cr_rs : nullptr, (long long)H * B2 * E, sy2,
-                       (long long)B2 * E, B2, 0, B2, HEAD_STORE, hc);
+                       (long long)B2 * E, B2, 0, B2, HEAD_STORE, hc, h->stream_bwd ? B : B2);
         } else {
             fwd_hidden(c, sM, N, tref(h->cr_in, (long long)Kc * B2, 0), B2, B2, h->cr_u, h->cr_h, sy2,
                        &h->cr_mu, &h->cr_rs, B2, true);
