@@ -1765,7 +1765,9 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
 #pragma unroll
                 for (int c = 0; c < 4; ++c) dh[r][c] *= gelu_grad_fast(u[r][c]);
         }
-        {
+        if (gp || g.da == nullptr) {
+            // du_l is the dW GEMMs' operand (grad columns) or input_grad_kernel's; the dQ/da
+            // columns of a fused backward need it only in LDS
             const rsrc_t rD = make_rsrc(g.DU[l] + dso, (long long)H * g.ld_d);
             const int vo = ((64 * w + 16 * lk) * g.ld_d + li) * 4;
 #pragma unroll
@@ -1775,6 +1777,11 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
                     bstore1(rD, dh[r][c], vo, (4 * r + c) * g.ld_d * 4);
                     slab_l[(4 * r + c) * NC] = dh[r][c];
                 }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) slab_l[(4 * r + c) * NC] = dh[r][c];
         }
         __syncthreads();
         if (gp) part[l * H + tid] = row_sum(slab);  // bias: sum du
