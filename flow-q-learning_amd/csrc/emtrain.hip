@@ -54,6 +54,7 @@ struct StepArgs {
     Net net, tpn;                       // trained net; frozen termination predictor (kind 0, tw > 0)
     const float* params;
     const float* tp;
+    const float *wt, *tpt;              // W^T copies of params / tp (Dense kernels [out][in], same offsets)
     float* part;                        // [blocks][P] partial grads
     long long P;
     float* logs;                        // [blocks][NLOG]
@@ -125,19 +126,19 @@ DEV void dense_fwd(const float* W, const float* b, const float* in, int K, int N
     __syncthreads();
 }
 
-// g_in[k][r] = sum_f W[k][f] g[f][r] (times relu'(in) when mask_in): thread = (k, row group)
+// g_in[k][r] = sum_f W[k][f] g[f][r] (times relu'(in) when mask_in): thread = (k, row group).
+// WT = W^T [N][K] (the transposed copy the optimiser keeps): lanes read consecutive k.
 template <int RPT>
-DEV void dense_dx_t(const float* __restrict__ W, const float* g, int K, int N, float* g_in, const float* mask_in) {
+DEV void dense_dx_t(const float* __restrict__ WT, const float* g, int K, int N, float* g_in, const float* mask_in) {
     constexpr int RG = R / RPT;
     for (int t = threadIdx.x; t < K * RG; t += NT) {
         const int k = t % K, r0 = (t / K) * RPT;
         float acc[RPT];
 #pragma unroll
         for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
-        const float* __restrict__ wr = W + (long long)k * N;
 #pragma unroll 4
         for (int f = 0; f < N; ++f) {
-            const float w = wr[f];
+            const float w = WT[(long long)f * K + k];
             const float* x = g + f * R + r0;
 #pragma unroll
             for (int r = 0; r < RPT; ++r) acc[r] = fmaf(w, x[r], acc[r]);
@@ -150,12 +151,12 @@ DEV void dense_dx_t(const float* __restrict__ W, const float* g, int K, int N, f
         }
     }
 }
-DEV void dense_dx(const float* W, const float* g, int K, int N, float* g_in, const float* mask_in) {
-    if (K * 16 <= NT) dense_dx_t<1>(W, g, K, N, g_in, mask_in);
-    else if (K * 8 <= NT) dense_dx_t<2>(W, g, K, N, g_in, mask_in);
-    else if (K * 4 <= NT) dense_dx_t<4>(W, g, K, N, g_in, mask_in);
-    else if (K * 2 <= NT) dense_dx_t<8>(W, g, K, N, g_in, mask_in);
-    else dense_dx_t<16>(W, g, K, N, g_in, mask_in);
+DEV void dense_dx(const float* WT, const float* g, int K, int N, float* g_in, const float* mask_in) {
+    if (K * 16 <= NT) dense_dx_t<1>(WT, g, K, N, g_in, mask_in);
+    else if (K * 8 <= NT) dense_dx_t<2>(WT, g, K, N, g_in, mask_in);
+    else if (K * 4 <= NT) dense_dx_t<4>(WT, g, K, N, g_in, mask_in);
+    else if (K * 2 <= NT) dense_dx_t<8>(WT, g, K, N, g_in, mask_in);
+    else dense_dx_t<16>(WT, g, K, N, g_in, mask_in);
     __syncthreads();
 }
 
@@ -207,7 +208,7 @@ DEV void tp_score(const StepArgs& a, float* const* tacts, float* gA, float* gB, 
     float* src = gB;
     float* dst = gC;
     for (int i = T.n - 1; i >= 0; --i) {
-        dense_dx(a.tp + T.w[i], src, T.dims[i], T.dims[i + 1], dst, i > 0 ? tacts[i] : nullptr);
+        dense_dx(a.tpt + T.w[i], src, T.dims[i], T.dims[i + 1], dst, i > 0 ? tacts[i] : nullptr);
         float* tmp = src;
         src = dst;
         dst = tmp;
@@ -370,7 +371,7 @@ __global__ __launch_bounds__(NT) void em_grad_kernel(const StepArgs a) {
     float* gn = gB;
     for (int i = N.n - 1; i >= 0; --i) {
         dense_dw(acts[i], g, N.dims[i], N.dims[i + 1], pg + N.w[i], pg + N.b[i]);
-        if (i > 0 || N.ln_scale >= 0) dense_dx(P + N.w[i], g, N.dims[i], N.dims[i + 1], gn, i > 0 ? acts[i] : nullptr);
+        if (i > 0 || N.ln_scale >= 0) dense_dx(a.wt + N.w[i], g, N.dims[i], N.dims[i + 1], gn, i > 0 ? acts[i] : nullptr);
         else __syncthreads();
         float* tmp = g;
         g = gn;
@@ -537,7 +538,7 @@ __global__ __launch_bounds__(NT) void em_seq_grad_kernel(const StepArgs a) {
         float* gn = gB;
         for (int i = N.n - 1; i >= 0; --i) {
             dense_dw(acts[i], g, N.dims[i], N.dims[i + 1], pg + N.w[i], pg + N.b[i], acc);
-            dense_dx(P + N.w[i], g, N.dims[i], N.dims[i + 1], gn, i > 0 ? acts[i] : nullptr);
+            dense_dx(a.wt + N.w[i], g, N.dims[i], N.dims[i + 1], gn, i > 0 ? acts[i] : nullptr);
             float* tmp = g;
             g = gn;
             gn = tmp;
@@ -574,6 +575,8 @@ __global__ __launch_bounds__(NT) void em_seq_grad_kernel(const StepArgs a) {
 
 struct AdamArgsEm {
     float* params;
+    float* wt;                          // W^T copy, refreshed with the update
+    Net net;
     float *m, *v;
     const float* part;
     long long P;
@@ -591,7 +594,13 @@ __global__ __launch_bounds__(256) void em_adam_kernel(const AdamArgsEm a) {
     const float v = 0.001f * (g * g) + 0.999f * a.v[p];
     a.m[p] = m;
     a.v[p] = v;
-    a.params[p] = a.params[p] + (-a.lr) * ((m / a.bc1) / (sqrtf(v / a.bc2) + 1e-8f));
+    const float np = a.params[p] + (-a.lr) * ((m / a.bc1) / (sqrtf(v / a.bc2) + 1e-8f));
+    a.params[p] = np;
+    for (int i = 0; i < a.net.n; ++i) {
+        const long long o = p - a.net.w[i];
+        const int K = a.net.dims[i], N = a.net.dims[i + 1];
+        if (o >= 0 && o < (long long)K * N) a.wt[a.net.w[i] + (o % N) * K + o / N] = np;
+    }
 }
 
 }  // namespace em
@@ -653,6 +662,17 @@ Net layout(int in, int nh, const int* hid, int out, bool ln, long long* total) {
     *total = o;
     return n;
 }
+
+// Flat params with every Dense kernel [in][out] replaced by its transpose [out][in]
+std::vector<float> transposed(const Net& n, const float* p, long long P) {
+    std::vector<float> t(p, p + P);
+    for (int i = 0; i < n.n; ++i) {
+        const int K = n.dims[i], N = n.dims[i + 1];
+        for (int k = 0; k < K; ++k)
+            for (int f = 0; f < N; ++f) t[n.w[i] + (long long)f * K + k] = p[n.w[i] + (long long)k * N + f];
+    }
+    return t;
+}
 }  // namespace
 
 struct fqlpop_emtrain {
@@ -661,6 +681,7 @@ struct fqlpop_emtrain {
     Net net{}, tpn{};
     long long P = 0, PT = 0;
     float *params = nullptr, *m = nullptr, *v = nullptr, *part = nullptr, *logs = nullptr, *tp = nullptr;
+    float *wt = nullptr, *tpt = nullptr;  // W^T copies (the backward's dX reads)
     float *d_obs = nullptr, *d_act = nullptr, *d_rew = nullptr, *d_nobs = nullptr;
     long long n_rows = 0;
     float *i_obs = nullptr, *i_act = nullptr, *i_rew = nullptr, *i_nobs = nullptr;
@@ -677,7 +698,8 @@ struct fqlpop_emtrain {
 static void em_free(fqlpop_emtrain* h) {
     for (void* p : {(void*)h->params, (void*)h->m, (void*)h->v, (void*)h->part, (void*)h->logs, (void*)h->tp,
                     (void*)h->d_obs, (void*)h->d_act, (void*)h->d_rew, (void*)h->d_nobs, (void*)h->i_obs,
-                    (void*)h->i_act, (void*)h->i_rew, (void*)h->i_nobs, (void*)h->i_keep, (void*)h->seq})
+                    (void*)h->i_act, (void*)h->i_rew, (void*)h->i_nobs, (void*)h->i_keep, (void*)h->seq,
+                    (void*)h->wt, (void*)h->tpt})
         if (p) (void)hipFree(p);
     if (h->s) (void)hipStreamDestroy(h->s);
 }
@@ -755,6 +777,9 @@ int fqlpop_emtrain_create(const fqlpop_emtrain_config* cfg, const float* params,
         EMCHK(hipMalloc(&h->part, 4 * P * h->blocks));
         EMCHK(hipMalloc(&h->logs, 4 * (long long)NLOG * h->blocks));
         EMCHK(hipMemcpy(h->params, params, 4 * P, hipMemcpyHostToDevice));
+        EMCHK(hipMalloc(&h->wt, 4 * P));
+        const std::vector<float> wt = transposed(h->net, params, P);
+        EMCHK(hipMemcpy(h->wt, wt.data(), 4 * P, hipMemcpyHostToDevice));
         EMCHK(hipMemset(h->m, 0, 4 * P));
         EMCHK(hipMemset(h->v, 0, 4 * P));
         EMCHK(hipMemset(h->logs, 0, 4 * (long long)NLOG * h->blocks));
@@ -794,7 +819,10 @@ int fqlpop_emtrain_set_frozen_termination(fqlpop_emtrain_t* h, const float* tp_p
         EMARG(n == h->PT, "termination predictor size mismatch");
         EMCHK(hipSetDevice(h->device));
         if (!h->tp) EMCHK(hipMalloc(&h->tp, 4 * h->PT));
+        if (!h->tpt) EMCHK(hipMalloc(&h->tpt, 4 * h->PT));
         EMCHK(hipMemcpy(h->tp, tp_params, 4 * h->PT, hipMemcpyHostToDevice));
+        const std::vector<float> tt = transposed(h->tpn, tp_params, h->PT);
+        EMCHK(hipMemcpy(h->tpt, tt.data(), 4 * h->PT, hipMemcpyHostToDevice));
     });
 }
 
@@ -830,6 +858,8 @@ static StepArgs em_args(fqlpop_emtrain* h, bool train, bool injected) {
     a.tpn = h->tpn;
     a.params = h->params;
     a.tp = h->tp;
+    a.wt = h->wt;
+    a.tpt = h->tpt;
     a.part = h->part;
     a.P = h->P;
     a.logs = h->logs;
@@ -865,7 +895,7 @@ static void em_launch_step(fqlpop_emtrain* h, const StepArgs& a) {
     const auto& c = h->cfg;
     const double cc = (double)std::min<long long>(h->count, c.steps);
     AdamArgsEm ad{};
-    ad.params = h->params; ad.m = h->m; ad.v = h->v; ad.part = h->part;
+    ad.params = h->params; ad.wt = h->wt; ad.net = h->net; ad.m = h->m; ad.v = h->v; ad.part = h->part;
     ad.P = h->P; ad.blocks = h->blocks;
     ad.lr = (float)(c.init_lr * 0.5 * (1.0 + std::cos(3.14159265358979323846 * cc / c.steps)));
     ad.bc1 = (float)(1.0 - std::pow(0.9, (double)(h->count + 1)));
