@@ -17,9 +17,10 @@
 // two launches: em_grad_kernel (block = 16 minibatch rows: forward, loss,
 // backward, per-block partial parameter grads, per-block log sums; activations
 // in LDS, feature-major [feature][row]; the weights stream from L2) and
-// em_adam_kernel (fixed-order sum of the block partials + Adam).  VALU fp32 FMA
-// (each weight load feeds up to 16 rows): the layer widths (33, 28, 1) do not
-// tile onto MFMA shapes and the step is launch-latency bound anyway.
+// em_adam_kernel (fixed-order sum of the block partials + Adam, which also
+// refreshes the W^T copy the dX products read).  Every Dense product (forward,
+// dX, dW) runs on v_mfma_f32_16x16x4_f32 with the block's 16 rows as the MFMA
+// width; odd widths (33, 28, 1) are padded by the buffer loads' range check.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -95,84 +96,95 @@ DEV float urand(uint64_t seed, uint32_t a, uint32_t b, uint32_t c) {
 
 DEV float softplus(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
 
-// out[f][r] = act(sum_k W[k][f] in[k][r] + b[f]) for f < N, r < R; thread = (f, row group).
-template <int RPT>
-DEV void dense_fwd_t(const float* __restrict__ W, const float* __restrict__ bias, const float* in, int K, int N,
-                     float* out, bool relu) {
-    constexpr int RG = R / RPT;
-    for (int t = threadIdx.x; t < N * RG; t += NT) {
-        const int f = t % N, r0 = (t / N) * RPT;
-        float acc[RPT];
-        const float bf = bias[f];
+// Dense layers on v_mfma_f32_16x16x4_f32: out[m][c] = act(sum_k A[k][m] x[k][c] + bias[m])
+// for m < M, c < R = 16 (LDS, feature-major [m][R]); A is k-major [Kr][M] (m contiguous).
+// A block's 8 waves take 16-feature output tiles round-robin; a wave loads the A
+// fragments of KS k-steps (4 k each, up to 32) into registers at once (all in flight: the loop is
+// L2-latency bound otherwise), then runs the MFMAs with x from LDS.  Forward: A = W
+// [K][N]; dX: A = W^T [N][K] with mask = relu'(the layer input).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+template <int KS>
+DEV void em_mfma_t(const float* __restrict__ A, const float* __restrict__ bias, const float* x, int Kr, int M,
+                   float* y, bool relu, const float* mask) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, lk = lane >> 4;
+    const int ntile = (M + 15) / 16, nks = (Kr + 3) / 4;
+    // unguarded buffer loads (a guarded load compiles to a branch + vmcnt(0) wait): k >= Kr
+    // falls past the range and reads 0; a lane's o >= M only feeds its own discarded row
+    const rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, Kr * M * 4, 0x00020000);
+    for (int t = w; t < ntile; t += NT / 64) {
+        const int o = 16 * t + li;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s0 = 0; s0 < nks; s0 += KS) {
+            float av[KS];
 #pragma unroll
-        for (int r = 0; r < RPT; ++r) acc[r] = bf;
-#pragma unroll 4
-        for (int k = 0; k < K; ++k) {
-            const float w = W[(long long)k * N + f];
-            const float* x = in + k * R + r0;
+            for (int u = 0; u < KS; ++u)
+                av[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                      rA, ((4 * (s0 + u) + lk) * M + o) * 4, 0, 0));
 #pragma unroll
-            for (int r = 0; r < RPT; ++r) acc[r] = fmaf(w, x[r], acc[r]);
+            for (int u = 0; u < KS; ++u) {
+                if (s0 + u < nks) {
+                    const int k = 4 * (s0 + u) + lk;
+                    const float xv = x[min(k, Kr - 1) * R + li];
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], k < Kr ? xv : 0.f, acc, 0, 0, 0);
+                }
+            }
         }
+        // acc[r]: output m = 16t + 4lk + r, column li
 #pragma unroll
-        for (int r = 0; r < RPT; ++r) out[f * R + r0 + r] = relu ? fmaxf(acc[r], 0.f) : acc[r];
+        for (int r = 0; r < 4; ++r) {
+            const int m = 16 * t + 4 * lk + r;
+            if (m < M) {
+                float v = acc[r] + (bias ? bias[m] : 0.f);
+                if (relu) v = fmaxf(v, 0.f);
+                if (mask && !(mask[m * R + li] > 0.f)) v = 0.f;  // relu' (0 at 0)
+                y[m * R + li] = v;
+            }
+        }
     }
+    __syncthreads();
 }
+DEV void em_mfma(const float* A, const float* bias, const float* x, int Kr, int M, float* y, bool relu,
+                 const float* mask) {
+    if (Kr <= 32) em_mfma_t<8>(A, bias, x, Kr, M, y, relu, mask);
+    else if (Kr <= 64) em_mfma_t<16>(A, bias, x, Kr, M, y, relu, mask);
+    else em_mfma_t<32>(A, bias, x, Kr, M, y, relu, mask);
+}
+// out[f][r] = act(sum_k W[k][f] in[k][r] + b[f])
 DEV void dense_fwd(const float* W, const float* b, const float* in, int K, int N, float* out, bool relu) {
-    if (N * 16 <= NT) dense_fwd_t<1>(W, b, in, K, N, out, relu);
-    else if (N * 8 <= NT) dense_fwd_t<2>(W, b, in, K, N, out, relu);
-    else if (N * 4 <= NT) dense_fwd_t<4>(W, b, in, K, N, out, relu);
-    else if (N * 2 <= NT) dense_fwd_t<8>(W, b, in, K, N, out, relu);
-    else dense_fwd_t<16>(W, b, in, K, N, out, relu);
-    __syncthreads();
+    em_mfma(W, b, in, K, N, out, relu, nullptr);
 }
-
-// g_in[k][r] = sum_f W[k][f] g[f][r] (times relu'(in) when mask_in): thread = (k, row group).
-// WT = W^T [N][K] (the transposed copy the optimiser keeps): lanes read consecutive k.
-template <int RPT>
-DEV void dense_dx_t(const float* __restrict__ WT, const float* g, int K, int N, float* g_in, const float* mask_in) {
-    constexpr int RG = R / RPT;
-    for (int t = threadIdx.x; t < K * RG; t += NT) {
-        const int k = t % K, r0 = (t / K) * RPT;
-        float acc[RPT];
-#pragma unroll
-        for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
-#pragma unroll 4
-        for (int f = 0; f < N; ++f) {
-            const float w = WT[(long long)f * K + k];
-            const float* x = g + f * R + r0;
-#pragma unroll
-            for (int r = 0; r < RPT; ++r) acc[r] = fmaf(w, x[r], acc[r]);
-        }
-#pragma unroll
-        for (int r = 0; r < RPT; ++r) {
-            float v = acc[r];
-            if (mask_in && !(mask_in[k * R + r0 + r] > 0.f)) v = 0.f;  // relu' (0 at 0)
-            g_in[k * R + r0 + r] = v;
-        }
-    }
-}
+// g_in[k][r] = sum_f W[k][f] g[f][r] (times relu'(in) when mask_in), from WT = W^T [N][K]
+// (the transposed copy the optimiser keeps)
 DEV void dense_dx(const float* WT, const float* g, int K, int N, float* g_in, const float* mask_in) {
-    if (K * 16 <= NT) dense_dx_t<1>(WT, g, K, N, g_in, mask_in);
-    else if (K * 8 <= NT) dense_dx_t<2>(WT, g, K, N, g_in, mask_in);
-    else if (K * 4 <= NT) dense_dx_t<4>(WT, g, K, N, g_in, mask_in);
-    else if (K * 2 <= NT) dense_dx_t<8>(WT, g, K, N, g_in, mask_in);
-    else dense_dx_t<16>(WT, g, K, N, g_in, mask_in);
-    __syncthreads();
+    em_mfma(WT, nullptr, g, N, K, g_in, false, mask_in);
 }
 
-// Partial parameter grads of one Dense over the block's rows:
+// Partial parameter grads of one Dense over the block's rows (MFMA over the 16 rows):
 // dW[k][f] = sum_r in[k][r] g[f][r], db[f] = sum_r g[f][r]
 // (acc: added to the partials already there -- the sum over the steps of a sequence)
 DEV void dense_dw(const float* in, const float* g, int K, int N, float* __restrict__ pW, float* __restrict__ pb,
                   bool acc = false) {
-    for (int t = threadIdx.x; t < K * N; t += NT) {
-        const int k = t / N, f = t % N;
-        const float* a = in + k * R;
-        const float* b = g + f * R;
-        float s = 0.f;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, lk = lane >> 4;
+    const int tf = (N + 15) / 16, nt = (K + 15) / 16 * tf;
+    for (int t = w; t < nt; t += NT / 64) {
+        const int k0 = 16 * (t / tf), f0 = 16 * (t % tf);
+        f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < R; ++r) s = fmaf(a[r], b[r], s);
-        pW[t] = acc ? pW[t] + s : s;
+        for (int s = 0; s < R / 4; ++s) {
+            const float av = k0 + li < K ? in[(k0 + li) * R + 4 * s + lk] : 0.f;  // A[k][r]
+            const float bv = f0 + li < N ? g[(f0 + li) * R + 4 * s + lk] : 0.f;   // B[r][f]
+            d = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, d, 0, 0, 0);
+        }
+        // d[q]: k = k0 + 4lk + q, f = f0 + li
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = k0 + 4 * lk + q, f = f0 + li;
+            if (k < K && f < N) {
+                const long long o = (long long)k * N + f;
+                pW[o] = acc ? pW[o] + d[q] : d[q];
+            }
+        }
     }
     for (int f = threadIdx.x; f < N; f += NT) {
         const float* b = g + f * R;
