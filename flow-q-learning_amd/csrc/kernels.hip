@@ -2294,34 +2294,29 @@ bool rollout_supported(int H, int L, int D, int A) {
 }
 
 // y[o][c] = act(sum_k W[k][o] x[k][c] + b[o]), o < Wo, k < Wi, c < 16 (LDS in / out,
-// row pitch 16); res (optional, LDS [Wo][16]) is added after the activation.
-template <bool RELU>
-DEV void ro_dense(const float* __restrict__ W, const float* __restrict__ bias, const float* xin, int Wi, int Wo,
-                  float* yout, const float* res, int w, int li, int lk) {
+// row pitch 16); res (optional, LDS [Wo][16]) is added after the activation.  A wave
+// issues the W fragments of KS k-steps at once as unguarded buffer loads (k >= Wi reads 0
+// past the range; a lane's o >= Wo feeds only its own discarded row), then the MFMAs.
+template <bool RELU, int KS>
+DEV void ro_dense_t(const float* __restrict__ W, const float* __restrict__ bias, const float* xin, int Wi, int Wo,
+                    float* yout, const float* res, int w, int li, int lk) {
     const int ntile = (Wo + 15) / 16, nks = (Wi + 3) / 4;
+    const rsrc_t rW = make_rsrc(W, (long long)Wi * Wo);
     for (int t = w; t < ntile; t += EF_NW) {
         const int o = 16 * t + li;
-        const int oc = o < Wo ? o : Wo - 1;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        int s = 0;
-        for (; s + 4 <= nks; s += 4) {
-            float av[4], bv[4];
+        for (int s0 = 0; s0 < nks; s0 += KS) {
+            float av[KS];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int k = 4 * (s + u) + lk;
-                const int kc = k < Wi ? k : Wi - 1;
-                av[u] = (k < Wi && o < Wo) ? W[(long long)kc * Wo + oc] : 0.f;
-                bv[u] = k < Wi ? xin[kc * EF_NC + li] : 0.f;
+            for (int u = 0; u < KS; ++u) av[u] = bload1(rW, ((4 * (s0 + u) + lk) * Wo + o) * 4, 0);
+#pragma unroll
+            for (int u = 0; u < KS; ++u) {
+                if (s0 + u < nks) {
+                    const int k = 4 * (s0 + u) + lk;
+                    const float xv = xin[min(k, Wi - 1) * EF_NC + li];
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], k < Wi ? xv : 0.f, acc, 0, 0, 0);
+                }
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
-        }
-        for (; s < nks; ++s) {
-            const int k = 4 * s + lk;
-            const int kc = k < Wi ? k : Wi - 1;
-            const float av = (k < Wi && o < Wo) ? W[(long long)kc * Wo + oc] : 0.f;
-            const float bv = k < Wi ? xin[kc * EF_NC + li] : 0.f;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
         }
         // acc[r]: feature 16t + 4lk + r, column li
 #pragma unroll
@@ -2335,6 +2330,13 @@ DEV void ro_dense(const float* __restrict__ W, const float* __restrict__ bias, c
             }
         }
     }
+}
+template <bool RELU>
+DEV void ro_dense(const float* W, const float* bias, const float* xin, int Wi, int Wo, float* yout, const float* res,
+                  int w, int li, int lk) {
+    if (Wi <= 32) ro_dense_t<RELU, 8>(W, bias, xin, Wi, Wo, yout, res, w, li, lk);
+    else if (Wi <= 64) ro_dense_t<RELU, 16>(W, bias, xin, Wi, Wo, yout, res, w, li, lk);
+    else ro_dense_t<RELU, 32>(W, bias, xin, Wi, Wo, yout, res, w, li, lk);
 }
 
 __global__ __launch_bounds__(EF_NW * 64, 1) void rollout_kernel(const RolloutArgs g) {
