@@ -824,7 +824,11 @@ DEV void ef_kloop(f32x4 (&acc)[4], float4 (&ring)[PF], rsrc_t rW, const float* x
                   int w_next, int lo, int lk, int li) {
     constexpr int H = EF_H, NC = EF_NC;
     float bnext = xs[lk * NC + li];
-    for (int s0 = 0; s0 < NS; s0 += PF) {
+    // do-while (NS >= PF always): with no zero-trip path the waitcnt pass can prove that
+    // the loads issued before the loop (the caller's epilogue operands) are complete at
+    // the exit, instead of waiting there for the next layer's ring refills too
+    int s0 = 0;
+    do {
         // refill targets: k-steps s0+PF.. of this layer, or the next layer's first PF
         const int rbase = (s0 + PF < NS ? w_cur + 4 * (s0 + PF) * H : w_next) + lo;
 #pragma unroll
@@ -842,7 +846,8 @@ DEV void ef_kloop(f32x4 (&acc)[4], float4 (&ring)[PF], rsrc_t rW, const float* x
             ring[p] = bload4(rW, rbase + 4 * p * H);
             __builtin_amdgcn_sched_barrier(0);
         }
-    }
+        s0 += PF;
+    } while (s0 < NS);
 }
 
 bool euler_flow_supported(int H, int L, int D, int A, int B) {
