@@ -195,6 +195,28 @@ DEV void bstore1(rsrc_t r, float v, int voff_b, int soff_b) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, voff_b, soff_b, 0);
 }
 
+// Block prologue of the streamed kernels: in0[e] (e < EF_K0MAX*16 + 64) = rows [0, K0) of a
+// [K0][ld] input at columns c0 .. c0+15, zero below.  Unguarded buffer loads (rows >= K0
+// fall past the range and read 0), all issued before the first wait: a guarded load
+// compiles to a branch + vmcnt(0) each, which serialised this loop.
+template <int NT>
+DEV void load_in0(float* in0, const float* x, int K0, int ld, int c0) {
+    constexpr int N = 64 * 16 + 64, IT = (N + NT - 1) / NT;
+    static_assert(N >= 16, "");
+    const rsrc_t rX = make_rsrc(x, (long long)K0 * ld);
+    float v[IT];
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+        const int e = min((int)threadIdx.x + q * NT, N - 1), r = e >> 4, j = e & 15;
+        v[q] = bload1(rX, (r * ld + c0 + j) * 4, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+        const int e = (int)threadIdx.x + q * NT;
+        if (e < N) in0[e] = v[q];
+    }
+}
+
 // Global -> register staging of one operand slice.  An "IC" (i-contiguous)
 // operand slice is BK rows (r) x TILE cols (i); an "RC" slice is TILE rows (i)
 // x BK cols (r).  Element p of the thread's float4 list.
@@ -877,17 +899,17 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
     const int K0 = D + A + 1, NS0 = (K0 + 4 * PF - 1) / (4 * PF) * PF;  // padded k-steps of layer 0
     const float* __restrict__ P = g.params + (long long)slot * g.P;
     const float* __restrict__ eu = at(g.eu, slot);
-    for (int e = tid; e < EF_K0MAX * NC + 64; e += NT) {
-        const int r = e / NC, j = e % NC;
-        in0[e] = (r < D + A) ? eu[(long long)r * B + c0 + j] : 0.f;
-    }
+    load_in0<NT>(in0, eu, D + A, B, c0);
     if (tid < A) b5s[tid] = P[g.b_off[L] + tid];
-    // head A fragments (constant over the flow): W_L[64w + 4s + lk][li], li < A
+    const rsrc_t rW = make_rsrc(P, g.P);
+    // head A fragments (constant over the flow): W_L[64w + 4s + lk][li], li < A (unguarded
+    // loads inside the arena, then a select)
     float w5r[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) w5r[s] = li < A ? P[g.w_off[L] + (64 * w + 4 * s + lk) * A + li] : 0.f;
+    for (int s = 0; s < 16; ++s) w5r[s] = bload1(rW, ((int)g.w_off[L] + (64 * w + 4 * s + lk) * A + li) * 4, 0);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) w5r[s] = li < A ? w5r[s] : 0.f;
 
-    const rsrc_t rW = make_rsrc(P, g.P);
     const int lo = lk * H + 64 * w + 4 * li;
     float4 ring[PF];
 #pragma unroll
@@ -1181,10 +1203,7 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
     const int NS0 = (K0 + 4 * PF - 1) / (4 * PF) * PF;
     const float* __restrict__ P = g.params + (long long)slot * g.P + (long long)y * g.ens;
     const float* __restrict__ x0 = g.x0 + (long long)slot * g.x0_ss;
-    for (int e = tid; e < EF_K0MAX * NC + 64; e += NT) {
-        const int r = e / NC, j = e % NC;
-        in0[e] = r < K0 ? x0[(long long)r * g.ld_x + c0 + j] : 0.f;
-    }
+    load_in0<NT>(in0, x0, K0, g.ld_x, c0);
     const rsrc_t rW = make_rsrc(P, g.P);
     const int lo = lk * H + 64 * w + 4 * li;
     float4 ring[PF];
@@ -1631,7 +1650,16 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         const int j = tid / NC, col = tid % NC;
         dos[j][col] = g.dout[(long long)slot * g.dout_ss + (long long)y * g.dout_sy + (long long)j * g.ld_o + c0 + col];
     }
-    for (int e = tid; e < H * nout; e += NT) scr[e] = P[g.w_off[L] + e];
+    {
+        // head kernel W_L [H][nout] (nout <= 8): unguarded loads (past H*nout: 0), then stores
+        const rsrc_t rH = make_rsrc(P + g.w_off[L], (long long)H * nout);
+        float hv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) hv[q] = bload1(rH, (tid + q * NT) * 4, 0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (tid + q * NT < H * nout) scr[tid + q * NT] = hv[q];
+    }
     // W^T ring: the first PF k-steps of the first dX product (W_{L-1}^T)
     const int lo = lk * H + 64 * w + 4 * li;
     float4 ring[PF];
