@@ -1645,6 +1645,10 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
     const long long sto = (long long)slot * g.st_ss + (long long)y * g.st_sy + g.coff + c0;
     const long long dso = (long long)slot * g.d_ss + (long long)y * g.d_sy + c0;
     float* __restrict__ part = gp ? g.part + ((long long)(slot * g.ny + y) * (g.Mg / NC) + tile) * g.NP : nullptr;
+    // block-uniform buffer resources + 32-bit lane offsets for the per-layer accesses (no
+    // 64-bit per-lane addresses to keep live across the layer loop)
+    const rsrc_t rPart = make_rsrc(gp ? part : g.params, gp ? g.NP : 0);
+    const rsrc_t rPe = make_rsrc(P, g.ens);
 
     if (tid < nout * NC) {
         const int j = tid / NC, col = tid % NC;
@@ -1714,9 +1718,9 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
 #pragma unroll
             for (int c = 0; c < 4; ++c) u[r][c] = bload1(rU, vo, (4 * r + c) * g.ld_s * 4);
         if constexpr (LN) {
-            mu = g.MU[l][sto + li];
-            rs = g.RS[l][sto + li];
-            gth = P[g.g_off[l] + tid];
+            mu = bload1(make_rsrc(g.MU[l] + sto, NC), li * 4, 0);
+            rs = bload1(make_rsrc(g.RS[l] + sto, NC), li * 4, 0);
+            gth = bload1(rPe, tid * 4, (int)g.g_off[l] * 4);
         }
     };
     load_epi(L - 1);
@@ -1775,8 +1779,8 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
                 colred[1][w][li] = s2;
             }
             if (gp) {
-                part[(2 * L + l) * H + tid] = row_sum(scr);  // LN bias: sum dh
-                part[(L + l) * H + tid] = row_sum(slab);     // LN scale: sum dh * xhat
+                bstore1(rPart, row_sum(scr), tid * 4, (2 * L + l) * H * 4);   // LN bias: sum dh
+                bstore1(rPart, row_sum(slab), tid * 4, (L + l) * H * 4);      // LN scale: sum dh * xhat
             }
             __syncthreads();  // colred visible; scr, slab free
             float c1 = 0.f, c2 = 0.f;
@@ -1817,7 +1821,7 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
                 for (int c = 0; c < 4; ++c) slab_l[(4 * r + c) * NC] = dh[r][c];
         }
         __syncthreads();
-        if (gp) part[l * H + tid] = row_sum(slab);  // bias: sum du
+        if (gp) bstore1(rPart, row_sum(slab), tid * 4, l * H * 4);  // bias: sum du
         if (l == 0 && g.da != nullptr && !gp) {
             // dQ/da for the actor's Q-loss columns (replaces input_grad_kernel): output (j, col)
             // = thread & 127, feature quarter = thread >> 7, then a fixed-order fold in scr
