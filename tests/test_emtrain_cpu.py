@@ -231,3 +231,25 @@ def test_multistep_one_step_is_the_baseline_step():
     for m in g0:
         for k in g0[m]:
             np.testing.assert_allclose(g1[m][k], g0[m][k], rtol=1e-12, atol=1e-15)
+
+
+def test_multistep_loader_windows_like_reference():
+    """train_env_model.MultistepLoader = utils/data_loader.py:25-39: [n/1000][1000] episodes,
+    windows of T consecutive steps inside one episode, start in [0, 1000 - T)."""
+    import train_env_model as tem
+    n, D, A, T = 3000, 3, 2, 16
+    rows = np.arange(n, dtype=np.float32)
+    ds = {"observations": np.repeat(rows[:, None], D, 1), "actions": np.zeros((n, A), np.float32),
+          "rewards": rows.copy(), "next_observations": np.repeat(rows[:, None] + 1, D, 1)}
+    ld = tem.MultistepLoader(ds, T)
+    assert ld.dataset["observations"].shape == (3, 1000, D) and ld.dataset["rewards"].shape == (3, 1000)
+    np.random.seed(1)
+    b = ld.sample(64)
+    assert b["observations"].shape == (64, T, D) and b["rewards"].shape == (64, T)
+    first = b["rewards"][:, 0]
+    np.testing.assert_array_equal(b["rewards"], first[:, None] + np.arange(T))  # consecutive steps
+    start = first % 1000
+    assert (start >= 0).all() and (start < 1000 - T).all()  # never crosses an episode boundary
+    np.testing.assert_array_equal(b["next_observations"][..., 0], b["rewards"] + 1)
+    with pytest.raises(ValueError):
+        tem.MultistepLoader({k: v[:2500] for k, v in ds.items()}, T)
