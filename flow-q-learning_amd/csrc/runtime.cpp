@@ -203,6 +203,7 @@ struct fqlpop {
     unsigned long long* probe_slots = nullptr;   // [2 sets][pairs][probe_blocks][2]
     int probe_pairs = 0;
     long long probe_blocks = 0;                  // max blocks of one dominant-kernel launch
+    int probe_nz[2] = {0, 0};                    // active members of the step that used each set
     hipEvent_t probe_done[2] = {nullptr, nullptr};
     hipStream_t probe_stream = nullptr;
     bool probe_pending[2] = {false, false};
@@ -824,7 +825,9 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     hipStream_t sM = h->sM, sF = h->sF, sB = h->sB, sX = h->sX;
     h->ev_next = 0;
     h->probe_idx = 0;
-    if (h->probe_set >= 0)
+    // the persistent Euler launch writes both stamps of every block it launches, and the
+    // reduction reads only those (probe_nz): no per-step clearing node at the step's head
+    if (h->probe_set >= 0 && !h->euler_fused)
         HIPCHK(hipMemsetAsync(h->probe_slots + 2LL * h->probe_blocks * h->probe_set * h->probe_pairs, 0,
                               sizeof(unsigned long long) * 2 * h->probe_blocks * h->probe_pairs, sM));
 
@@ -1161,7 +1164,8 @@ void probe_consume(fqlpop* h, int set) {
                           hipMemcpyDeviceToHost, h->probe_stream));
     HIPCHK(hipStreamSynchronize(h->probe_stream));
     for (int p = 0; p < h->probe_pairs; ++p) {
-        const double us = probe_launch_us(v.data() + per * p, h->probe_blocks);
+        const long long nb = h->euler_fused ? h->probe_blocks / h->n * h->probe_nz[set] : h->probe_blocks;
+        const double us = probe_launch_us(v.data() + per * p, nb);
         if (us < 0) continue;  // launch not probed
         h->probe_total_ms += us * 1e-3;
         ++h->probe_launches;
@@ -1501,6 +1505,7 @@ int fqlpop_step(fqlpop_t* h, int n_steps) {
                 const int set = (int)(h->probe_step & 1);
                 if (h->probe_pending[set]) probe_consume(h, set);  // the step i-2 that used this set
                 h->probe_set = set;
+                h->probe_nz[set] = h->nz;
                 run(h, true, false, false);
                 h->probe_set = -1;
                 HIPCHK(hipEventRecord(h->probe_done[set], h->sM));
