@@ -1869,8 +1869,18 @@ __global__ __launch_bounds__(256) void colsum_reduce_kernel(const ColsumArgs a) 
     if (p >= a.NP) return;
     const int slot = a.slots[z];
     const float* __restrict__ src = a.part + (long long)(slot * a.ny + y) * a.tiles * a.NP + p;
+    // fixed tile order; 8 loads in flight per batch (one load per iteration waited on each
+    // partial separately)
     float s = 0.f;
-    for (int t = 0; t < a.tiles; ++t) s += src[(long long)t * a.NP];
+    int t = 0;
+    for (; t + 8 <= a.tiles; t += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[(long long)(t + u) * a.NP];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; t < a.tiles; ++t) s += src[(long long)t * a.NP];
     const int LH = a.L * a.H;
     const int reg = p < LH ? 0 : !a.ln ? 3 : p < 2 * LH ? 1 : p < 3 * LH ? 2 : 3;
     const int pr = reg == 3 ? p - (a.ln ? 3 : 1) * LH : p - reg * LH;

@@ -1062,6 +1062,10 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     if (train) {
         const NetLayout& N = h->os;
         if (h->fused_adam) {
+            // the critic's dW launch waits for the actor loss too, so that the actor backward
+            // (the critical chain) is dispatched first: a dW launch dispatched ahead of it
+            // takes every CU's LDS (3 blocks of 51 KB) and starves it
+            dep(sM, h->cdw_sb ? sB : sX);
             // actor dX chain, then the critic's grads + Adam (sX) beside the
             // actor's (sM), then the join
             std::function<void()> os_dw;

@@ -145,7 +145,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("FQLPOP_LIB") or LIB_PATH  # FQLPOP_LIB: A/B builds (developer)
     if not os.path.exists(p):
         raise FqlpopError(
             f"{p} not found: build the HIP extension first "
