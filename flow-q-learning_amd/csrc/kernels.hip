@@ -2013,8 +2013,10 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
     }
     const float* pn = a.inj_noise ? a.inj_noise + z * (long long)B * (4 * A + 1) : nullptr;
     const float t = pn ? pn[(long long)B * 2 * A + b] : u01(c0[1]);
-    for (int k = p; k < D; k += SP) {
-        const float o = obs[k], n = nobs[k];
+    // the row's observation features: the first KQ per thread with every load issued before
+    // the first wait (a loop that loads per iteration waits once per iteration; k clamped,
+    // stores guarded), any beyond (D > KQ * SP) one by one
+    auto put = [&](int k, float o, float n) {
         os[k * B3 + b] = n;
         os[k * B3 + B + b] = o;
         os[k * B3 + 2 * B + b] = o;
@@ -2024,7 +2026,19 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
         cr[k * B2 + B + b] = o;
         tg[(long long)k * B + b] = n;
         eu[(long long)k * B + b] = o;
+    };
+    constexpr int KQ = 8;
+    float ov[KQ], nv0[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+        const int k = min(p + SP * q, D - 1);
+        ov[q] = obs[k];
+        nv0[q] = nobs[k];
     }
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+        if (p + SP * q < D) put(p + SP * q, ov[q], nv0[q]);
+    for (int k = p + SP * KQ; k < D; k += SP) put(k, obs[k], nobs[k]);
     if (p < A) {
         const float av = actp[p];
         cr[(D + p) * B2 + b] = av;
