@@ -200,7 +200,8 @@ struct fqlpop {
     int probe_set = -1;            // set used by the step being enqueued (-1: none)
     int probe_idx = 0;             // next launch slot of that set
     long long probe_step = 0;
-    unsigned long long* probe_slots = nullptr;   // [2 sets][pairs][probe_blocks][2]
+    unsigned long long* probe_slots = nullptr;   // [2 sets][pairs][probe_blocks][2] (device view)
+    unsigned long long* probe_host = nullptr;    // the same slots: mapped coherent host memory
     int probe_pairs = 0;
     long long probe_blocks = 0;                  // max blocks of one dominant-kernel launch
     int probe_nz[2] = {0, 0};                    // active members of the step that used each set
@@ -1164,9 +1165,7 @@ void probe_consume(fqlpop* h, int set) {
     HIPCHK(hipEventSynchronize(h->probe_done[set]));
     const long long per = 2 * h->probe_blocks;
     std::vector<unsigned long long> v(per * h->probe_pairs);
-    HIPCHK(hipMemcpyAsync(v.data(), h->probe_slots + per * set * h->probe_pairs, sizeof(unsigned long long) * v.size(),
-                          hipMemcpyDeviceToHost, h->probe_stream));
-    HIPCHK(hipStreamSynchronize(h->probe_stream));
+    std::memcpy(v.data(), h->probe_host + per * set * h->probe_pairs, sizeof(unsigned long long) * v.size());
     for (int p = 0; p < h->probe_pairs; ++p) {
         const long long nb = h->euler_fused ? h->probe_blocks / h->n * h->probe_nz[set] : h->probe_blocks;
         const double us = probe_launch_us(v.data() + per * p, nb);
@@ -1328,8 +1327,12 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             h->probe_pairs = std::max(1, (cfg->flow_steps - 1) * (cfg->num_hidden - 1));
             h->probe_blocks = (long long)((cfg->hidden_dim + 63) / 64) * ((cfg->batch_size + 63) / 64) * n_members;
         }
-        HIPCHK(hipMalloc(&h->probe_slots, sizeof(unsigned long long) * 4 * h->probe_blocks * h->probe_pairs));
-        HIPCHK(hipMemset(h->probe_slots, 0, sizeof(unsigned long long) * 4 * h->probe_blocks * h->probe_pairs));
+        // the stamps go straight to mapped host memory: the host reads them after the step's
+        // event, with no device-to-host copy (a copy kernel) interleaved with the steps
+        const size_t pb = sizeof(unsigned long long) * 4 * h->probe_blocks * h->probe_pairs;
+        HIPCHK(hipHostMalloc((void**)&h->probe_host, pb, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(h->probe_host, 0, pb);
+        HIPCHK(hipHostGetDevicePointer((void**)&h->probe_slots, h->probe_host, 0));
         for (auto& e : h->probe_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHK(hipStreamCreateWithFlags(&h->probe_stream, hipStreamNonBlocking));
         for (auto& e : h->ev_pool) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1447,7 +1450,7 @@ int fqlpop_destroy(fqlpop_t* h) {
         for (hipEvent_t e : h->probe_done)
             if (e) (void)hipEventDestroy(e);
         if (h->probe_stream) (void)hipStreamDestroy(h->probe_stream);
-        if (h->probe_slots) (void)hipFree(h->probe_slots);
+        if (h->probe_host) (void)hipHostFree(h->probe_host);
         if (h->sX && h->sX != h->sM) (void)hipStreamDestroy(h->sX);
         if (h->sF && h->sF != h->sM) (void)hipStreamDestroy(h->sF);
         if (h->sB && h->sB != h->sM) (void)hipStreamDestroy(h->sB);
@@ -1806,7 +1809,7 @@ int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* 
         HIPCHK(hipEventSynchronize(h->ev_t1));
         HIPCHK(hipEventElapsedTime(&ms, h->ev_t0, h->ev_t1));
         std::vector<unsigned long long> v(2 * h->probe_blocks);
-        HIPCHK(hipMemcpy(v.data(), h->probe_slots, sizeof(unsigned long long) * v.size(), hipMemcpyDeviceToHost));
+        std::memcpy(v.data(), h->probe_host, sizeof(unsigned long long) * v.size());
         h->clock_check_event_us = 1000.0 * ms;
         h->clock_check_stamp_us = probe_launch_us(v.data(), h->probe_blocks);
     });
