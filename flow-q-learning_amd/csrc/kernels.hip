@@ -1307,7 +1307,9 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
     {
         float w5r[16];  // A fragments: W_L[64w + 4s + lk][li], li < nout
 #pragma unroll
-        for (int s = 0; s < 16; ++s) w5r[s] = li < nout ? P[g.w_off[L] + (64 * w + 4 * s + lk) * nout + li] : 0.f;
+        for (int s = 0; s < 16; ++s) w5r[s] = bload1(rW, ((int)g.w_off[L] + (64 * w + 4 * s + lk) * nout + li) * 4, 0);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) w5r[s] = li < nout ? w5r[s] : 0.f;  // unguarded loads, then a select
         f32x4 hacc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 16; ++s)
