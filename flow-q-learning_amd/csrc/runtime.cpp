@@ -65,6 +65,22 @@ void philox_host(uint32_t c[4], uint32_t k0, uint32_t k1) {
     }
 }
 
+// Sampler key of a member: its seed mixed with the bits of its alpha (splitmix64
+// finaliser).  The reference draws every experiment's batches from the global
+// np.random stream (trainer/trainer.py:76-81, [EXT] Dataset.sample), so two members
+// that share a seed but not an alpha see different batches there; keying the device
+// sampler by the seed alone would give them identical minibatches, flow times and
+// noises.  Independent of the slot, so a resumed or re-slotted member draws the same
+// stream.
+uint64_t sample_key(uint64_t seed, float alpha) {
+    uint32_t ab;
+    std::memcpy(&ab, &alpha, sizeof(ab));
+    uint64_t z = seed ^ ((uint64_t)ab << 32 | 0x9E3779B9u);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
 // ---------------------------------------------------------------- layout
 // Parameter block of one network, flax MLP naming: Dense_l (kernel [in][out],
 // bias [out]) and LayerNorm_l (scale, bias) after every hidden Dense.
@@ -135,6 +151,7 @@ struct fqlpop {
     float *grads = nullptr, *adam_m = nullptr, *adam_v = nullptr, *target = nullptr;
     int* count = nullptr;
     uint64_t* seeds = nullptr;
+    uint64_t* skeys = nullptr;  // per-member sampler key: sample_key(seed, alpha)
     float* alpha = nullptr;
     int* slots = nullptr;
     float* stats = nullptr;
@@ -364,6 +381,11 @@ void build_chunks(fqlpop* h) {
 void mirror_params(fqlpop* h, int slot, hipStream_t s) {
     HIPCHK(hipMemcpyAsync(h->params_nx + (long long)slot * h->P, h->params + (long long)slot * h->P,
                           sizeof(float) * h->P, hipMemcpyDeviceToDevice, s));
+}
+
+void upload_skey(fqlpop* h, int member) {
+    const uint64_t k = sample_key(h->h_seeds[member], h->h_alpha[member]);
+    HIPCHK(hipMemcpy(h->skeys + member, &k, sizeof(k), hipMemcpyHostToDevice));
 }
 
 void init_member(fqlpop* h, int slot, uint64_t seed) {
@@ -839,7 +861,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     sa.n_rows = dset.rows;
     sa.inj_batch = inj_batch ? h->inj_batch : nullptr;
     sa.inj_noise = inj_noise ? h->inj_noise : nullptr;
-    sa.seeds = h->seeds; sa.count = h->count;
+    sa.seeds = h->skeys; sa.count = h->count;
     sa.stream_salt = train ? 0x51A7u : 0x5A1Du;
     sa.B = B; sa.D = D; sa.A = A;
     sa.os_in = tref(h->os_in, (long long)Kc * B3);
@@ -1355,6 +1377,7 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         HIPCHK(hipMemset(h->grads, 0, sizeof(float) * h->P * n));
         HIPCHK(hipMalloc(&h->count, sizeof(int) * n));
         HIPCHK(hipMalloc(&h->seeds, sizeof(uint64_t) * n));
+        HIPCHK(hipMalloc(&h->skeys, sizeof(uint64_t) * n));
         HIPCHK(hipMalloc(&h->alpha, sizeof(float) * n));
         HIPCHK(hipMalloc(&h->slots, sizeof(int) * n));
         build_chunks(h.get());
@@ -1420,6 +1443,7 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         h->h_seeds.assign(seeds_in, seeds_in + n);
         HIPCHK(hipMemcpy(h->alpha, alphas, sizeof(float) * n, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(h->seeds, seeds_in, sizeof(uint64_t) * n, hipMemcpyHostToDevice));
+        for (int i = 0; i < n; ++i) upload_skey(h.get(), i);
         for (int i = 0; i < n; ++i) init_member(h.get(), i, seeds_in[i]);
         h->active.assign(n, 1);
         update_slots(h.get());
@@ -1437,7 +1461,7 @@ int fqlpop_destroy(fqlpop_t* h) {
             if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
         for (float* p : h->allocs) (void)hipFree(p);
         for (void* p : {(void*)h->params_buf[0], (void*)h->params_buf[1], (void*)h->res_ids, (void*)h->grads, (void*)h->adam_m, (void*)h->adam_v, (void*)h->target,
-                        (void*)h->count, (void*)h->seeds, (void*)h->alpha, (void*)h->slots, (void*)h->stats,
+                        (void*)h->count, (void*)h->seeds, (void*)h->skeys, (void*)h->alpha, (void*)h->slots, (void*)h->stats,
                         (void*)h->chunks, (void*)h->chunk_leaf, (void*)h->leaf_first, (void*)h->sp_params,
                         (void*)h->tp_params})
             if (p) (void)hipFree(p);
@@ -1730,6 +1754,7 @@ int fqlpop_set_member(fqlpop_t* h, int member, float alpha, uint64_t seed, int r
         h->h_seeds[member] = seed;
         HIPCHK(hipMemcpy(h->alpha + member, &alpha, sizeof(float), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(h->seeds + member, &seed, sizeof(uint64_t), hipMemcpyHostToDevice));
+        upload_skey(h, member);
         if (reinit) init_member(h, member, seed);
     });
 }

@@ -239,7 +239,9 @@ class _GpuEnvModelTrainer:
             if self.logger:
                 self.logger.log({"train/learning_rate": self.learning_rate(step),
                                  **{f"train/{k}": v for k, v in logs.items()}}, step=step)
-        self._val(self.config.steps)
+        # the reference logs the final pass at the last loop index (step = steps - 1,
+        # state_predictor_trainer.py:160-175), so the val curves line up when overlaid
+        self._val(self.config.steps - 1)
 
     def close(self):
         if getattr(self, "_h", None):

@@ -34,7 +34,11 @@ class Trainer:
         self.config = config
         self.experiments = {}
         self.member_of = {}
-        initial = list(state_dict["experiments"]) if state_dict else list(strategy.sample())
+        # strategy.sample() is called once on a fresh start (trainer/trainer.py:37-40 of the
+        # reference): the same set sizes the population and becomes the candidates, so a
+        # strategy whose sample() is stateful or random places the configs it returned
+        sampled = None if state_dict else strategy.sample()
+        initial = list(state_dict["experiments"]) if state_dict else list(sampled)
         self.population = self._make_population(initial, device)
         if state_dict is not None:
             for cfg, exp_state in state_dict["experiments"].items():
@@ -47,7 +51,7 @@ class Trainer:
         else:
             self.untrained_candidates = []
             self.finished_candidates = []
-            self.candidates = strategy.sample()
+            self.candidates = sampled
             for cfg in self.candidates:
                 self.create_experiment(cfg)
 

@@ -278,3 +278,29 @@ def test_euler_fused_matches_per_layer_path(monkeypatch):
         infos.append(pop.read_info("train")[0])
     for k in O.TRAIN_INFO_KEYS:
         assert _close(infos[0][k], infos[1][k], rel=2e-5), (k, infos[0][k], infos[1][k])
+
+
+def test_same_seed_members_with_different_alphas_draw_different_batches():
+    """The device sampler is keyed by (seed, alpha): two members sharing a seed
+    (tune_alpha.py's default --number_of_seeds=1 gives every alpha the same seed)
+    draw different minibatches, as the reference's members do from the global
+    np.random stream.  Step 1's critic statistics depend only on the batch and the
+    (identical, same-seed) initial parameters, so they must differ; a member keyed
+    like another (same seed and alpha) draws bit-identical batches."""
+    H, B = 64, 64
+    rng = np.random.default_rng(4)
+    N = 5000
+    obs = rng.standard_normal((N, 28)).astype(np.float32)
+    rew = np.where(rng.uniform(size=N) < 0.05, 0.0, -1.0).astype(np.float32)
+    data = {"observations": obs, "actions": rng.uniform(-1, 1, (N, 5)).astype(np.float32),
+            "rewards": rew, "masks": (1.0 - (rew == 0)).astype(np.float32),
+            "next_observations": (obs + 0.05 * rng.standard_normal((N, 28))).astype(np.float32)}
+    pop = _pop(H, B, [3.0, 30.0, 3.0], [9, 9, 9])
+    pop.set_dataset(data)
+    assert np.array_equal(pop.get_flat(0), pop.get_flat(1))  # same seed -> same init
+    pop.step(1)
+    info = pop.read_info("train")
+    crit = ("critic/critic_loss", "critic/q_mean", "critic/q_max", "critic/q_min")
+    assert all(info[0][k] != info[1][k] for k in crit), (info[0], info[1])
+    assert all(info[0][k] == info[2][k] for k in crit)
+    assert np.array_equal(pop.get_flat(0), pop.get_flat(2))
