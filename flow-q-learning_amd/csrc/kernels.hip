@@ -257,13 +257,28 @@ constexpr int gemm_smem_floats() {
 // count+1) reading p from the current buffer and writing the other one, the
 // target EMA from the pre-update p (critic), grad stats.  The new p goes back
 // into the LDS tile, and a second pass writes W^T rows (float4 along i).
+// float4 global access, optionally non-temporal (a streamed optimiser operand read or
+// written once per step need not displace the weights the streamed kernels re-read)
+typedef float f32v4 __attribute__((ext_vector_type(4)));
+DEV float4 ld4(const float* p, int nt) {
+    if (nt) {
+        const f32v4 v = __builtin_nontemporal_load(reinterpret_cast<const f32v4*>(p));
+        return float4{v.x, v.y, v.z, v.w};
+    }
+    return *reinterpret_cast<const float4*>(p);
+}
+DEV void st4(float* p, float4 v, int nt) {
+    if (nt) __builtin_nontemporal_store(f32v4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32v4*>(p));
+    else *reinterpret_cast<float4*>(p) = v;
+}
+
 template <int BM, int BN, bool DUAL>
 DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc)[BM / 64][BN / 64],
                        f32x16 (&acc2)[BM / 64][BN / 64], int slot, int y, int tile, int per, int i0, int j0,
                        int wi, int wj, int l32, int lh, float* smem) {
     constexpr int TM = BM / 64, TN = BN / 64;
     constexpr int PT = BN + 1;  // LDS row pitch (odd: the transposed read of pass 2 spreads over banks)
-    static_assert(BM * PT <= gemm_smem_floats<BM, BN, 32, true, true>(), "gradient tile must fit the operand LDS");
+    // (the launching kernel sizes smem for the gradient tile: group_smem_floats)
     const int gM = g.M, ldc = g.ldc, tid = threadIdx.x;
     __syncthreads();  // every wave is done with the operand buffers
 #pragma unroll
@@ -288,6 +303,7 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
     const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
     const float rbc1 = 1.0f / bc1, rbc2 = 1.0f / bc2;
     const float lr = e.lr, tau = e.tau;
+    const int nt = e.nt;
     float mx = -INFINITY, mn = INFINITY, ss = 0.f;
     const int rows = e.mode == 1 ? 0 : min(BM, gM - i0);  // mode 1: timing probe only (no optimiser traffic)
     // pass 1: thread -> 4 consecutive columns of a row; U iterations in flight
@@ -300,10 +316,10 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
             const int i = r0 + u * RPI + ri;
             if (i < rows) {
                 const long long o = (long long)(i0 + i) * ldc + j0 + cj;
-                p4[u] = *reinterpret_cast<const float4*>(Pi + o);
-                m4[u] = *reinterpret_cast<const float4*>(Mm + o);
-                v4[u] = *reinterpret_cast<const float4*>(Vv + o);
-                if (Tt) t4[u] = *reinterpret_cast<const float4*>(Tt + o);
+                p4[u] = ld4(Pi + o, nt & 4);
+                m4[u] = ld4(Mm + o, nt & 1);
+                v4[u] = ld4(Vv + o, nt & 1);
+                if (Tt) t4[u] = ld4(Tt + o, nt & 2);
             }
         }
 #pragma unroll
@@ -331,10 +347,10 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
                     mn = fminf(mn, gr);
                     ss += gr * gr;
                 }
-                *reinterpret_cast<float4*>(Po + o) = float4{pp[0], pp[1], pp[2], pp[3]};
-                *reinterpret_cast<float4*>(Mm + o) = float4{mm[0], mm[1], mm[2], mm[3]};
-                *reinterpret_cast<float4*>(Vv + o) = float4{vv[0], vv[1], vv[2], vv[3]};
-                if (Tt) *reinterpret_cast<float4*>(Tt + o) = float4{tt[0], tt[1], tt[2], tt[3]};
+                st4(Po + o, float4{pp[0], pp[1], pp[2], pp[3]}, nt & 8);
+                st4(Mm + o, float4{mm[0], mm[1], mm[2], mm[3]}, nt & 1);
+                st4(Vv + o, float4{vv[0], vv[1], vv[2], vv[3]}, nt & 1);
+                if (Tt) st4(Tt + o, float4{tt[0], tt[1], tt[2], tt[3]}, nt & 2);
             }
         }
     }
@@ -356,8 +372,7 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
         for (int q = tid; q < BM * BN / 4; q += 256) {
             const int jj = q / TPC, ii = (q % TPC) * 4;
             const float* src = smem + ii * PT + jj;
-            *reinterpret_cast<float4*>(WT + (long long)(j0 + jj) * gM + i0 + ii) =
-                float4{src[0], src[PT], src[2 * PT], src[3 * PT]};
+            st4(WT + (long long)(j0 + jj) * gM + i0 + ii, float4{src[0], src[PT], src[2 * PT], src[3 * PT]}, nt & 8);
         }
     }
 }
@@ -527,9 +542,18 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
 
 // Grouped launch of independent problems of one layout (the dW GEMMs of every
 // layer of a network): block -> problem by the prefix of tile counts.
-template <int BM, int BN, bool ARC, bool BRC, int EPI = EPI_STORE>
+// LDS of a grouped dW launch: the operand double buffer, or the fused optimiser's
+// gradient tile (BM rows of BN + 1) when that is larger (BK = 16 slices)
+template <int BM, int BN, int BK, bool ARC, bool BRC, int EPI>
+constexpr int group_smem_floats() {
+    return (EPI == EPI_ADAM && BM * (BN + 1) > gemm_smem_floats<BM, BN, BK, ARC, BRC>())
+               ? BM * (BN + 1)
+               : gemm_smem_floats<BM, BN, BK, ARC, BRC>();
+}
+
+template <int BM, int BN, bool ARC, bool BRC, int EPI = EPI_STORE, int BK = 32>
 __global__ __launch_bounds__(256, 2) void gemm_group_kernel(const GemmGroupArgs ga) {
-    __shared__ __attribute__((aligned(16))) float smem[gemm_smem_floats<BM, BN, 32, ARC, BRC>()];
+    __shared__ __attribute__((aligned(16))) float smem[group_smem_floats<BM, BN, BK, ARC, BRC, EPI>()];
     if (EPI == EPI_ADAM && (int)blockIdx.x >= ga.first[ga.ng]) {
         // the net's small leaves: raw block ids past the tiles (the dispatcher spreads
         // consecutive ids over the XCDs, so they add no per-XCD imbalance)
@@ -542,7 +566,7 @@ __global__ __launch_bounds__(256, 2) void gemm_group_kernel(const GemmGroupArgs 
 #pragma unroll
     for (int i = 1; i < GEMM_GROUP_MAX; ++i)
         if (i < ga.ng && bid >= ga.first[i]) gi = i;
-    gemm_body<BM, BN, 32, false, ARC, BRC, EPI>(ga.g[gi], bid - ga.first[gi], smem, &ga.adam, gi);
+    gemm_body<BM, BN, BK, false, ARC, BRC, EPI>(ga.g[gi], bid - ga.first[gi], smem, &ga.adam, gi);
 }
 
 int gemm_group_tiles(int tile, int M, int N) {
@@ -563,15 +587,16 @@ void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, c
     if (adam) {
         ga.adam = *adam;
         tot += adam->small_blocks;
-        switch (tile) {
+        switch (tile == 6 ? 6 : tile & 3) {
             case 0: hipLaunchKernelGGL((gemm_group_kernel<64, 64, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga); break;
             case 1: hipLaunchKernelGGL((gemm_group_kernel<128, 64, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga); break;
             case 2: hipLaunchKernelGGL((gemm_group_kernel<64, 128, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga); break;
+            case 6: hipLaunchKernelGGL((gemm_group_kernel<64, 128, true, true, EPI_ADAM, 16>), dim3(tot), dim3(256), 0, s, ga); break;
             default: hipLaunchKernelGGL((gemm_group_kernel<128, 128, true, true, EPI_ADAM>), dim3(tot), dim3(256), 0, s, ga); break;
         }
         return;
     }
-    switch (tile) {
+    switch (tile & 3) {  // (BK 16 only in the fused-optimiser launch)
         case 0: hipLaunchKernelGGL((gemm_group_kernel<64, 64, true, true>), dim3(tot), dim3(256), 0, s, ga); break;
         case 1: hipLaunchKernelGGL((gemm_group_kernel<128, 64, true, true>), dim3(tot), dim3(256), 0, s, ga); break;
         case 2: hipLaunchKernelGGL((gemm_group_kernel<64, 128, true, true>), dim3(tot), dim3(256), 0, s, ga); break;

@@ -214,6 +214,8 @@ struct fqlpop {
     RolloutArgs em_args{};
     bool em_set = false;
     bool probe = false;
+    int pipe_exp = 0;
+    bool pipe_started = false;  // FQLPOP_PIPE_EXP timing experiment (eager, racy)
     int probe_set = -1;            // set used by the step being enqueued (-1: none)
     int probe_idx = 0;             // next launch slot of that set
     long long probe_step = 0;
@@ -301,14 +303,16 @@ long long leaf_member_size(const NetLayout& N, int kind, int layer) {
     return N.H;
 }
 
-// dW group tile of a net (stream_bwd_net; 0 = 64x64, 1 = 128x64, 2 = 64x128, 3 = 128x128)
+// dW group tile of a net (stream_bwd_net; 0 = 64x64, 1 = 128x64, 2 = 64x128, 3 = 128x128,
+// + 4: k-slices of 16 instead of 32 in the fused-optimiser launch)
 // (64 x 128 for every net: with the fused optimiser epilogue, 3 blocks per CU
 // overlap one block's HBM-bound epilogue with the others' k-loops better than
-// 2 blocks of 128 x 128; FQLPOP_DW_TILE_C / _A override, for measurements)
+// 2 blocks of 128 x 128.  BK = 16: 26 KB of LDS and 129 VGPRs instead of 51 KB and
+// 146, +0.6 % same-box; FQLPOP_DW_TILE_C / _A override, for measurements)
 int dw_tile(const NetLayout& N) {
     const char* t = std::getenv(N.E > 1 ? "FQLPOP_DW_TILE_C" : "FQLPOP_DW_TILE_A");
     if (t) return std::atoi(t);
-    return 2;
+    return 6;
 }
 
 void build_chunks(fqlpop* h) {
@@ -698,6 +702,11 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         {
             const char* dm = std::getenv("FQLPOP_DW_MODE");
             ae.mode = dm ? std::atoi(dm) : 0;
+            // m, v and the target stream non-temporally: read and written once per step, they
+            // need not displace the weights the streamed kernels re-read from L2 / MALL
+            // (+1.0 % same-box; FQLPOP_ADAM_NT: bit mask, see AdamEpi::nt)
+            const char* nt = std::getenv("FQLPOP_ADAM_NT");
+            ae.nt = nt ? std::atoi(nt) : 3;
         }
         ae.small = adam_args(c, ni);
         ae.small_blocks = ae.small.n_chunks * c.nz;
@@ -874,10 +883,21 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     sa.rew_t = tref(h->rew_t, B);
     sa.mask_t = tref(h->mask_t, B);
     sa.nz = c.nz; sa.slots = h->slots;
-    launch_sample(sa, sM);
-    HIPCHK(hipEventRecord(h->ev_sample, sM));
-    HIPCHK(hipStreamWaitEvent(sF, h->ev_sample, 0));
-    HIPCHK(hipStreamWaitEvent(sB, h->ev_sample, 0));
+    if (h->pipe_exp && train) {
+        // TIMING EXPERIMENT ONLY (results are racy): the next step's sampling, BC forward
+        // and flow wait only for the previous step's BC optimiser
+        if (h->pipe_started) HIPCHK(hipStreamWaitEvent(sF, h->pipe_exp == 2 ? h->ev_t1 : h->ev_bdone, 0));
+        launch_sample(sa, sF);
+        HIPCHK(hipEventRecord(h->ev_sample, sF));
+        HIPCHK(hipStreamWaitEvent(sM, h->ev_sample, 0));
+        HIPCHK(hipStreamWaitEvent(sB, h->ev_sample, 0));
+        h->pipe_started = true;
+    } else {
+        launch_sample(sa, sM);
+        HIPCHK(hipEventRecord(h->ev_sample, sM));
+        HIPCHK(hipStreamWaitEvent(sF, h->ev_sample, 0));
+        HIPCHK(hipStreamWaitEvent(sB, h->ev_sample, 0));
+    }
 
     float* info = train ? h->info : h->vinfo;
     LossArgs la{};
@@ -1082,6 +1102,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
     HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
     launch_loss_actor(la, sM);
+    if (h->pipe_exp == 2 && train) HIPCHK(hipEventRecord(h->ev_t1, sM));
     if (train) {
         const NetLayout& N = h->os;
         if (h->fused_adam) {
@@ -1317,6 +1338,10 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             h->sF = h->sB = h->sX = h->sM;
         }
         h->ev_pool.resize(64);
+        {
+            const char* pe = std::getenv("FQLPOP_PIPE_EXP");
+            h->pipe_exp = pe && !cfg->use_graph ? std::atoi(pe) : 0;
+        }
         {
             const char* ef = std::getenv("FQLPOP_EULER");
             h->euler_fused = euler_flow_supported(H, L, D, A, B) && !h->bc.ln && !(ef && std::atoi(ef) == 0);
