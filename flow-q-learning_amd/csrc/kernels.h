@@ -375,7 +375,7 @@ struct RolloutArgs {
     const float* init_obs;         // [n_envs][D]
     int n_envs, max_steps;
     uint64_t seed;
-    const uint64_t* member_seeds;  // per slot
+    const uint64_t* member_seeds;  // per slot: the member key sample_key(seed, alpha) (runtime.cpp)
     const float* noise;            // null or [nz][max_steps][n_envs][A]
     float* out;                    // [nz][n_envs][2]: success, episode length
     float* out_obs;                // null or [nz][n_envs][D]: observation after the last step

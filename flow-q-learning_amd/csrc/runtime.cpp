@@ -2005,7 +2005,7 @@ int fqlpop_rollout(fqlpop_t* h, const float* init_obs, int n_envs, int max_steps
         for (int l = 0; l <= h->L; ++l) { r.w_off[l] = h->os.W[l]; r.b_off[l] = h->os.b[l]; }
         r.D = D; r.A = A; r.L = h->L;
         r.sp = h->sp_params; r.tp = h->tp_params;
-        r.n_envs = n_envs; r.max_steps = max_steps; r.seed = seed; r.member_seeds = h->seeds;
+        r.n_envs = n_envs; r.max_steps = max_steps; r.seed = seed; r.member_seeds = h->skeys;
         r.nz = nz; r.slots = h->slots;
         float *d_obs = nullptr, *d_noise = nullptr, *d_out = nullptr, *d_oobs = nullptr;
         const size_t n_noise = (size_t)nz * max_steps * n_envs * A;
@@ -2040,7 +2040,7 @@ int fqlpop_envmodel_step(fqlpop_t* h, const float* obs, const float* actions, in
         r.params = h->params; r.P = h->P; r.os_off = h->os.off;
         r.D = D; r.A = A; r.L = h->L;
         r.sp = h->sp_params; r.tp = h->tp_params;
-        r.n_envs = n; r.max_steps = 1; r.seed = 0; r.member_seeds = h->seeds;
+        r.n_envs = n; r.max_steps = 1; r.seed = 0; r.member_seeds = h->skeys;
         r.nz = 1; r.slots = h->slots;  // any slot: the actor is not run
         float *d_obs = nullptr, *d_act = nullptr, *d_out = nullptr, *d_oobs = nullptr, *d_logit = nullptr;
         HIPCHK(hipMalloc(&d_obs, sizeof(float) * n * D));

@@ -65,3 +65,99 @@ def max_over_ranks(value: float, device: torch.device | None = None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+# ------------------------------------------------------------------ halving
+# A population sharded over ranks (BASELINE configs 4 and 5): every
+# rank holds the same HPO strategy and takes the same decisions from the gathered
+# scores, trains only the members it owns, and hands members to other ranks when
+# pruning leaves the shards uneven.  Everything below is a pure function of the
+# (identical) strategy state, so all ranks compute the same owners and moves
+# without exchanging them.
+
+def config_key(cfg):
+    """Total order on ExperimentConfig-like records (alpha, then seed; None first),
+    the order every rank iterates candidates in."""
+    def k(v):
+        return (0, 0.0) if v is None else (1, float(v))
+    return (k(getattr(cfg, "alpha", None)), k(getattr(cfg, "seed", None)))
+
+
+def ordered(configs):
+    return sorted(configs, key=config_key)
+
+
+def assign_owners(configs, world_size: int) -> dict:
+    """Round-robin over the ordered candidates: config -> rank."""
+    return {c: i % world_size for i, c in enumerate(ordered(configs))}
+
+
+def shard_capacity(n_configs: int, world_size: int) -> int:
+    """Population slots a rank needs: its initial share, which pruning and
+    rebalancing never exceed."""
+    return max(1, -(-n_configs // world_size))
+
+
+def rebalance_plan(live, owner: dict, world_size: int) -> list:
+    """Moves (config, src, dst) that even out the live members per rank (max - min
+    <= 1), moving the fewest members: while uneven, the last live config (in
+    ``ordered`` order) of the most loaded rank goes to the least loaded one (lowest
+    rank id on ties)."""
+    shards = {r: [c for c in ordered(live) if owner[c] == r] for r in range(world_size)}
+    moves = []
+    while True:
+        hi = max(range(world_size), key=lambda r: (len(shards[r]), -r))
+        lo = min(range(world_size), key=lambda r: (len(shards[r]), r))
+        if len(shards[hi]) - len(shards[lo]) <= 1:
+            return moves
+        c = shards[hi].pop()
+        shards[lo].append(c)
+        moves.append((c, hi, lo))
+
+
+def place_new(new_configs, live, owner: dict, world_size: int) -> dict:
+    """Owners for configs a strategy adds: each goes to the currently least loaded rank."""
+    load = {r: sum(1 for c in live if owner.get(c) == r) for r in range(world_size)}
+    out = {}
+    for c in ordered(new_configs):
+        r = min(range(world_size), key=lambda q: (load[q], q))
+        out[c] = r
+        load[r] += 1
+    return out
+
+
+def broadcast_object(obj, src: int = 0):
+    """``obj`` of rank ``src`` on every rank."""
+    rank, ws = world()
+    if ws == 1:
+        return obj
+    box = [obj if rank == src else None]
+    dist.broadcast_object_list(box, src=src)
+    return box[0]
+
+
+def send_object(obj, dst: int) -> None:
+    dist.send_object_list([obj], dst=dst)
+
+
+def recv_object(src: int):
+    box = [None]
+    dist.recv_object_list(box, src=src)
+    return box[0]
+
+
+def gather_objects(obj, dst: int = 0):
+    """List of every rank's ``obj`` on rank ``dst`` (None elsewhere)."""
+    rank, ws = world()
+    if ws == 1:
+        return [obj]
+    out = [None] * ws if rank == dst else None
+    dist.gather_object(obj, out, dst=dst)
+    return out
+
+
+def eval_round_seed(base_seed: int, round_index: int) -> int:
+    """Seed of the world-model evaluation of round ``round_index``: a function of
+    the run seed and the round only, so a member's scores do not depend on the
+    sharding (the single-process Trainer draws it from the global np.random)."""
+    return int(np.random.default_rng([int(base_seed) & 0xFFFFFFFF, int(round_index)]).integers(0, 2**31 - 1))

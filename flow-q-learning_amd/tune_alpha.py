@@ -7,7 +7,14 @@ the whole population (here: all members together on the GPU) and writes
 <save>/<env>/checkpoint.pkl.  --strategy successive_halving selects halving.
 
 Data: --task synthetic (default; SURVEY.md 8d transitions + a toy evaluation
-env) or --task npz (local OGBench .npz files under --data_directory).
+env), --task npz (local OGBench .npz files under --data_directory) or --task
+simulated (candidates scored by world-model rollouts on the GPU).
+
+Multi-GPU (BASELINE configs 4 / 5): launched by torch.distributed.run with one
+process per GPU (``python -m torch.distributed.run --nproc-per-node 8
+--master-addr 127.0.0.1 tune_alpha.py ...``), the population is sharded over the
+ranks by trainer.distributed_trainer.DistributedTrainer (RCCL over xGMI gathers
+the scores and moves members after pruning); rank 0 writes the checkpoint.
 """
 from __future__ import annotations
 
@@ -30,6 +37,15 @@ from trainer.trainer import Trainer  # noqa: E402
 
 
 def make_task(args, config):
+    if args.task == "simulated":
+        # world-model evaluation on the GPU (BASELINE config 5): the reference's env-model files
+        # under <save>/<env>/env_models if present, else a seeded synthetic model
+        from task.offline_task_simulated import OfflineTaskWithSimulatedEvaluations
+        env_dir = config.save_directory / config.env_name / "env_models"
+        return OfflineTaskWithSimulatedEvaluations(
+            config.env_name, model=args.env_model, save_directory=config.save_directory if env_dir.exists() else None,
+            n_rows=args.synthetic_rows, num_evaluation_envs=config.eval_episodes,
+            max_episode_steps=args.max_episode_steps, seed=config.seed)
     if args.task == "npz":
         from task.offline_task_npz import OfflineTaskNpz
         return OfflineTaskNpz(config.env_name, config.data_directory)
@@ -43,13 +59,26 @@ def main(argv=None):
     parser.add_argument("--max_evaluations", type=int, default=200)
     parser.add_argument("--number_of_seeds", type=int, default=1)
     parser.add_argument("--number_of_alphas", type=int, default=1)
-    parser.add_argument("--task", choices=("synthetic", "npz"), default="synthetic")
+    parser.add_argument("--task", choices=("synthetic", "npz", "simulated"), default="synthetic")
+    parser.add_argument("--env_model", choices=("baseline", "multistep"), default="multistep")
+    parser.add_argument("--max_episode_steps", type=int, default=1000)
     parser.add_argument("--synthetic_rows", type=int, default=100_000)
     parser.add_argument("--strategy", choices=("identity", "successive_halving"), default="identity")
     parser.add_argument("--fraction", type=float, default=0.5)
     parser.add_argument("--history_length", type=int, default=1)
     args = parser.parse_args(argv)
     config = build_config_from_args(args)
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    device = 0
+    if world_size > 1 and not args.single_experiment:
+        import torch
+        import torch.distributed as dist
+        device = int(os.environ.get("LOCAL_RANK", "0"))
+        if torch.cuda.is_available():
+            torch.cuda.set_device(device)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
 
     random.seed(config.seed)
     np.random.seed(config.seed)
@@ -80,11 +109,21 @@ def main(argv=None):
         strategy = SuccessiveHalving(population=set(configs), total_evaluations=args.max_evaluations,
                                      fraction=args.fraction, history_length=args.history_length,
                                      state_dict=state.get("strategy"))
-    trainer = Trainer(task, strategy, config, state_dict=state.get("trainer"))
+    if world_size > 1:
+        from trainer.distributed_trainer import DistributedTrainer
+        trainer = DistributedTrainer(task, strategy, config, state_dict=state.get("trainer"), device=device)
+    else:
+        trainer = Trainer(task, strategy, config, state_dict=state.get("trainer"))
     trainer.train(max_evaluations=args.max_evaluations)
-    ckpt.parent.mkdir(parents=True, exist_ok=True)
-    with open(ckpt, "wb") as f:
-        pickle.dump({"trainer": trainer.state_dict(), "strategy": trainer.strategy.state_dict()}, f)
+    trainer_state = trainer.state_dict()  # collective under DistributedTrainer (rank 0 gets it)
+    if trainer_state is not None:
+        ckpt.parent.mkdir(parents=True, exist_ok=True)
+        with open(ckpt, "wb") as f:
+            pickle.dump({"trainer": trainer_state, "strategy": trainer.strategy.state_dict()}, f)
+    if world_size > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
