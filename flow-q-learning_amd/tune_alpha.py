@@ -73,11 +73,14 @@ def main(argv=None):
     if world_size > 1 and not args.single_experiment:
         import torch
         import torch.distributed as dist
-        device = int(os.environ.get("LOCAL_RANK", "0"))
-        if torch.cuda.is_available():
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        n_dev = torch.cuda.device_count()
+        if n_dev >= world_size:  # one GPU per rank: RCCL (the "nccl" backend) over xGMI
+            device = local_rank
             torch.cuda.set_device(device)
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
+        else:  # fewer GPUs than ranks (a rehearsal on a small box): ranks share GPUs, gloo
+            device = local_rank % max(n_dev, 1)
             dist.init_process_group("gloo")
 
     random.seed(config.seed)

@@ -145,6 +145,44 @@ def test_tune_alpha_driver(tmp_path):
     assert len(ckpts) >= 1
 
 
+def test_tune_alpha_two_ranks_and_resume(tmp_path):
+    """tune_alpha.py under torch.distributed.run (2 ranks sharing this box's GPU, gloo):
+    halving over the world-model scores (4 candidates, 8 evaluations: milestones [4, 2],
+    so 4 -> 2 after the second round, when the budget is spent), rank 0 writes the
+    reference-shaped checkpoint, and a one-rank run resumes from it to the end."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = os.path.join(root, "flow-q-learning_amd", "tune_alpha.py")
+    args = [f"--save_directory={tmp_path}", "--steps=40", "--eval_interval=10", "--log_interval=10",
+            "--agent.batch_size=64", "--agent.layer_norm", "--eval_episodes=8", "--synthetic_rows=5000",
+            "--task=simulated", "--max_episode_steps=20", "--number_of_alphas=4", "--number_of_seeds=1",
+            "--strategy=successive_halving", "--fraction=0.5", "--history_length=1", "--max_evaluations=8"]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), script] + args,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    ckpt = tmp_path / "cube-single-play-singletask-task2-v0" / "checkpoint.pkl"
+
+    def load():
+        with open(ckpt, "rb") as f:
+            return pickle.load(f)
+    state = load()
+    tr = state["trainer"]
+    assert len(tr["experiments"]) == 4 and len(tr["candidates"]) == 2  # every member recorded, 2 pruned
+    assert all(tr["experiments"][c]["current_step"] == 20 for c in tr["candidates"])
+    assert tr["round_index"] == 2 and len(state["strategy"]["candidate_scores"]) == 4
+    import tune_alpha
+    tune_alpha.main(args)  # resume on one rank: the two survivors train to the end
+    tr = load()["trainer"]
+    assert len(tr["candidates"]) == 2 and set(tr["finished_candidates"]) == set(tr["candidates"])
+    assert all(tr["experiments"][c]["current_step"] == 40 for c in tr["candidates"])
+
+
 def test_integration_md_binding_stub():
     """The reference-side ctypes stub printed in INTEGRATION.md section 3 runs
     against the built library and agrees with the shipped surface."""
