@@ -163,6 +163,9 @@ struct fqlpop {
     // W_l tiles, and the remaining (small-leaf) chunks the adam kernel runs
     bool fused_adam = false;
     bool cdw_sb = true;            // the critic's fused dW + optimiser on sB (beside the actor chain)
+    int dwopt_mask = 0;            // nets (bit ni) whose fused dW + optimiser runs pipelined (launch_dwopt)
+    int dwopt_tpb[3] = {0, 0, 0};  // its tiles per block (0: 2 blocks per CU)
+    int n_cu = 256;
     int w_stat_base[3][EF_MAX_LAYERS] = {};
     int* res_ids = nullptr;
     int res_base[3] = {0, 0, 0}, res_n[3] = {0, 0, 0};
@@ -305,14 +308,15 @@ long long leaf_member_size(const NetLayout& N, int kind, int layer) {
 
 // dW group tile of a net (stream_bwd_net; 0 = 64x64, 1 = 128x64, 2 = 64x128, 3 = 128x128,
 // + 4: k-slices of 16 instead of 32 in the fused-optimiser launch)
-// (64 x 128 for every net: with the fused optimiser epilogue, 3 blocks per CU
+// (64 x 128 for every net: with the fused optimiser epilogue, more co-resident blocks
 // overlap one block's HBM-bound epilogue with the others' k-loops better than
-// 2 blocks of 128 x 128.  BK = 16: 26 KB of LDS and 129 VGPRs instead of 51 KB and
-// 146, +0.6 % same-box; FQLPOP_DW_TILE_C / _A override, for measurements)
+// 2 blocks of 128 x 128.  BK = 16: 33 KB of LDS and 129 VGPRs instead of 51 KB and
+// 146, +0.6 % same-box; 10 = the same at <= 128 VGPRs, 4 blocks per CU instead of 3,
+// +0.4 % same-box; FQLPOP_DW_TILE_C / _A override, for measurements)
 int dw_tile(const NetLayout& N) {
     const char* t = std::getenv(N.E > 1 ? "FQLPOP_DW_TILE_C" : "FQLPOP_DW_TILE_A");
     if (t) return std::atoi(t);
-    return 6;
+    return 10;
 }
 
 void build_chunks(fqlpop* h) {
@@ -710,7 +714,9 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         }
         ae.small = adam_args(c, ni);
         ae.small_blocks = ae.small.n_chunks * c.nz;
-        launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw, &ae);
+        if ((h->dwopt_mask & (1 << ni)) && (dw_tile(N) & 3) == 2)  // (its stats chunks: 64 x 128 tiles)
+            launch_dwopt(gs.data(), (int)gs.size(), sw, ae, h->dwopt_tpb[ni], h->n_cu);
+        else launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw, &ae);
     } else if (N.L <= GEMM_GROUP_MAX && N.H % 128 == 0) {
         launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw);
     } else {
@@ -1366,6 +1372,18 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             const char* fa = std::getenv("FQLPOP_FUSED_ADAM");
             h->fused_adam = h->stream_bwd && H % 128 == 0 && L <= GEMM_GROUP_MAX && h->critic.off == 0 &&
                             !(fa && std::atoi(fa) == 0);
+            // the pipelined form (optimiser of tile n inside the k-loop of tile n+1):
+            // FQLPOP_DWOPT = bit mask of nets (1 critic, 2 bc, 4 os), FQLPOP_DWOPT_TPB_{C,B,O}
+            const char* dp = std::getenv("FQLPOP_DWOPT");
+            h->dwopt_mask = h->fused_adam && dp ? std::atoi(dp) : 0;
+            const char* tn[3] = {"FQLPOP_DWOPT_TPB_C", "FQLPOP_DWOPT_TPB_B", "FQLPOP_DWOPT_TPB_O"};
+            for (int i = 0; i < 3; ++i) {
+                const char* v = std::getenv(tn[i]);
+                h->dwopt_tpb[i] = v ? std::atoi(v) : 0;
+            }
+            int ncu = 0;
+            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) == hipSuccess && ncu > 0)
+                h->n_cu = ncu;
         }
         if (h->euler_fused) {  // dominant kernel: one persistent Euler launch per step
             h->probe_pairs = 1;
