@@ -99,12 +99,7 @@ struct GemmGroupArgs {
     int first[GEMM_GROUP_MAX + 1];   // prefix of per-problem block counts
     int ng;
     AdamEpi adam;                    // used by the fused-Adam launch only
-    int nblk;                        // pipelined launch: persistent tile blocks (a multiple of 8)
 };
-// Pipelined fused dW + optimiser (64 x 128 tiles, BK 16): persistent blocks walk a
-// range of tiles; the optimiser / EMA / W^T passes of tile n run inside the
-// k-loop of tile n+1.  tpb: tiles per block (0: the whole chip at 2 blocks per CU).
-void launch_dwopt(const GemmArgs* gs, int ng, hipStream_t s, const AdamEpi& adam, int tpb, int n_cu);
 // tile: 2 = 64x128, 3 = 128x128 (others 64x64 / 128x64); adam != null: fused
 // optimiser epilogue (tile 2 or 3 only), else plain stores into g[i].C
 void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, const AdamEpi* adam = nullptr);

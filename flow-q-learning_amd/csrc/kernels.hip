@@ -15,8 +15,6 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
-#include <algorithm>
-#include <cstdlib>
 
 namespace fq {
 
@@ -618,358 +616,6 @@ void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, c
         case 2: hipLaunchKernelGGL((gemm_group_kernel<64, 128, true, true>), dim3(tot), dim3(256), 0, s, ga); break;
         default: hipLaunchKernelGGL((gemm_group_kernel<128, 128, true, true>), dim3(tot), dim3(256), 0, s, ga); break;
     }
-}
-
-// ------------------------------------------------ pipelined dW + optimiser --
-// The fused launch above runs each tile's k-loop and then its optimiser pass
-// (HBM-bound: p, m, v, target in and out, W^T out) back to back, so a block's
-// own loads wait out the HBM latency between its MFMA phases, and the two
-// phases overlap only where co-resident blocks happen to be out of step (about
-// half).  Here a block walks a range of tiles and runs the
-// optimiser of tile n in "units" (one float4 per thread each) inside the
-// k-loop of tile n+1: unit u is computed after iteration u's MFMAs, its HBM
-// loads were issued one iteration earlier (the loads do not depend on the
-// gradient, so unit 0's go out during tile n's own last iteration), and the
-// W^T units follow once every new p of the tile is in LDS.  The gradient tile
-// has its own LDS image (the operand double buffer stays live for the next
-// tile), 59 KB per block: 2 blocks per CU.  The last k-slice prefetch of a tile
-// loads the next tile's first slice, so the operand stream never drains.
-// Tiles: XCD x owns the contiguous range [T x / 8, T (x + 1) / 8) of the
-// group's linear tile index (as xcd_remap), its blocks interleave over it, so
-// concurrently running tiles share their operands in that XCD's L2.
-// Same arithmetic as adam_epilogue (same order per element), so the results
-// are bit-identical to the unpipelined launch.
-struct DwTile {
-    int gi, tile, per, y, slot, i0, j0, rows;
-};
-
-DEV DwTile dw_decode(const GemmGroupArgs& ga, int t) {
-    int gi = 0;
-#pragma unroll
-    for (int i = 1; i < GEMM_GROUP_MAX; ++i)
-        if (i < ga.ng && t >= ga.first[i]) gi = i;
-    const GemmArgs& g = ga.g[gi];
-    const int tiles_m = (g.M + 63) / 64, tiles_n = g.N / 128, per = tiles_m * tiles_n;
-    const int w = t - ga.first[gi];
-    DwTile d;
-    d.gi = gi;
-    d.per = per;
-    d.tile = w % per;
-    const int yz = w / per;
-    d.y = yz % g.ny;
-    d.slot = g.slots[yz / g.ny];
-    d.i0 = (d.tile / tiles_n) * 64;
-    d.j0 = (d.tile % tiles_n) * 128;
-    d.rows = min(64, g.M - d.i0);
-    return d;
-}
-
-// optimiser side of one tile (the "previous" tile while the next one's k-loop runs).
-// Plain pointers: buffer resources are built at each access (a resource kept in a
-// struct across the loop was demoted to memory and re-read through waterfall loops)
-struct DwOpt {
-    const float* pP;
-    float *pPo, *pM, *pV, *pT, *pWT;
-    int n, i0, j0, rows, gM, ldc, hasT, hasWT;
-    float rbc1, rbc2;
-    long long stat;  // element index of the tile's stats triple
-};
-
-DEV DwOpt dw_opt_ctx(const GemmGroupArgs& ga, const DwTile& d) {
-    const AdamEpi& e = ga.adam;
-    const GemmArgs& g = ga.g[d.gi];
-    DwOpt o;
-    o.n = g.M * g.ldc;  // the leaf: rows past M read 0 and their stores drop
-    const long long pb = (long long)d.slot * e.P + e.w_off[d.gi] + (long long)d.y * e.ens;
-    o.pP = e.p_in + pb;
-    o.pPo = e.p_out + pb;
-    o.pM = e.m + pb;
-    o.pV = e.v + pb;
-    o.hasT = e.target != nullptr;
-    o.pT = o.hasT ? e.target + (long long)d.slot * e.PT + e.w_off[d.gi] + (long long)d.y * e.ens : e.m + pb;
-    o.hasWT = e.wt_off[d.gi] >= 0;
-    o.pWT = o.hasWT ? e.wt_out + (long long)d.slot * e.PTT + e.wt_off[d.gi] + (long long)d.y * e.wt_sy : e.m + pb;
-    o.i0 = d.i0;
-    o.j0 = d.j0;
-    o.rows = d.rows;
-    o.gM = g.M;
-    o.ldc = g.ldc;
-    const float t = (float)(e.count[d.slot] + 1);
-    o.rbc1 = 1.0f / (1.0f - powf(0.9f, t));
-    o.rbc2 = 1.0f / (1.0f - powf(0.999f, t));
-    o.stat = ((long long)d.slot * e.n_total_chunks + e.stat_base[d.gi] + d.y * d.per + d.tile) * 3;
-    return o;
-}
-
-struct DwOptRegs {
-    float4 p, m, v, t;
-};
-
-constexpr int DW_AUX_NT = 2;  // buffer cache policy: non-temporal (m, v, target: read and written once a step)
-DEV float4 bload4_aux(rsrc_t r, int off_b, int nt) {
-    return __builtin_bit_cast(float4, nt ? __builtin_amdgcn_raw_buffer_load_b128(r, off_b, 0, DW_AUX_NT)
-                                         : __builtin_amdgcn_raw_buffer_load_b128(r, off_b, 0, 0));
-}
-DEV void bstore4_aux(rsrc_t r, float4 v, int off_b, int nt) {
-    const auto w = __builtin_bit_cast(__attribute__((ext_vector_type(4))) int, v);
-    if (nt) __builtin_amdgcn_raw_buffer_store_b128(w, r, off_b, 0, DW_AUX_NT);
-    else __builtin_amdgcn_raw_buffer_store_b128(w, r, off_b, 0, 0);
-}
-
-// unit u: float4 q = 256 u + tid of the 64 x 128 tile (row q / 32, columns 4 (q % 32) ..)
-DEV int dw_unit_off(const DwOpt& o, int u) {
-    const int q = u * 256 + (int)threadIdx.x;
-    return ((o.i0 + (q >> 5)) * o.ldc + o.j0 + (q & 31) * 4) * 4;
-}
-
-DEV void dw_opt_load(DwOptRegs& r, const DwOpt& o, int u) {
-    const int off = dw_unit_off(o, u);
-    r.p = bload4_aux(make_rsrc(o.pP, o.n), off, 0);
-    r.m = bload4_aux(make_rsrc(o.pM, o.n), off, 1);
-    r.v = bload4_aux(make_rsrc(o.pV, o.n), off, 1);
-    r.t = o.hasT ? bload4_aux(make_rsrc(o.pT, o.n), off, 1) : float4{0.f, 0.f, 0.f, 0.f};
-}
-
-constexpr int DW_PT = 128 + 1;  // gradient tile row pitch in LDS
-
-DEV void dw_opt_compute(const DwOptRegs& r, const DwOpt& o, int u, float* gt, float lr, float tau, float& mx,
-                        float& mn, float& ss) {
-    const int q = u * 256 + (int)threadIdx.x, row = q >> 5, cj = (q & 31) * 4;
-    float* gs = gt + row * DW_PT + cj;
-    float pp[4] = {r.p.x, r.p.y, r.p.z, r.p.w};
-    float mm[4] = {r.m.x, r.m.y, r.m.z, r.m.w};
-    float vv[4] = {r.v.x, r.v.y, r.v.z, r.v.w};
-    float tt[4] = {r.t.x, r.t.y, r.t.z, r.t.w};
-    const bool live = row < o.rows;  // rows past M (first layer): zero gradients, no stats
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const float gr = gs[c];
-        mm[c] = 0.1f * gr + 0.9f * mm[c];
-        vv[c] = 0.001f * (gr * gr) + 0.999f * vv[c];
-        const float mh = mm[c] * o.rbc1, vh = vv[c] * o.rbc2;
-        tt[c] = tau * pp[c] + (1.0f - tau) * tt[c];
-        pp[c] = pp[c] + (-lr) * (mh * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vh) + 1e-8f));
-        gs[c] = pp[c];
-        mx = live ? fmaxf(mx, gr) : mx;
-        mn = live ? fminf(mn, gr) : mn;
-        ss = live ? ss + gr * gr : ss;
-    }
-    const int off = dw_unit_off(o, u);
-    bstore4_aux(make_rsrc(o.pPo, o.n), float4{pp[0], pp[1], pp[2], pp[3]}, off, 0);
-    bstore4_aux(make_rsrc(o.pM, o.n), float4{mm[0], mm[1], mm[2], mm[3]}, off, 1);
-    bstore4_aux(make_rsrc(o.pV, o.n), float4{vv[0], vv[1], vv[2], vv[3]}, off, 1);
-    if (o.hasT) bstore4_aux(make_rsrc(o.pT, o.n), float4{tt[0], tt[1], tt[2], tt[3]}, off, 1);
-}
-
-// W^T unit u (hidden layers, M = H): W^T[j0 + jj][i0 + ii .. +3] from the new p in LDS
-DEV void dw_wt_unit(const DwOpt& o, int u, const float* gt) {
-    const int q = u * 256 + (int)threadIdx.x, jj = q >> 4, ii = (q & 15) * 4;
-    const float* src = gt + ii * DW_PT + jj;
-    bstore4_aux(make_rsrc(o.pWT, o.n), float4{src[0], src[DW_PT], src[2 * DW_PT], src[3 * DW_PT]},
-                ((o.j0 + jj) * o.gM + o.i0 + ii) * 4, 0);
-}
-
-// every unit of a tile, not overlapped (small K, and the block's last tile)
-DEV void dw_drain(const DwOpt& o, float* gt, float lr, float tau, float& mx, float& mn, float& ss) {
-    constexpr int NOPT = 8;
-#pragma unroll
-    for (int u0 = 0; u0 < NOPT; u0 += 4) {
-        DwOptRegs r[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dw_opt_load(r[k], o, u0 + k);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dw_opt_compute(r[k], o, u0 + k, gt, lr, tau, mx, mn, ss);
-    }
-    __syncthreads();
-    if (o.hasWT) {
-#pragma unroll
-        for (int u = 0; u < NOPT; ++u) dw_wt_unit(o, u, gt);
-    }
-}
-
-DEV void dw_finish(const DwOpt& o, float* stats, float mx, float mn, float ss, float* red) {
-    mx = block_max(mx, red);
-    mn = block_min(mn, red);
-    ss = block_sum(ss, red);
-    if (threadIdx.x == 0) {
-        float* st = stats + o.stat;
-        st[0] = mx;
-        st[1] = mn;
-        st[2] = ss;
-    }
-}
-
-template <int DWD>
-__global__ __launch_bounds__(256, 2) void dwopt_kernel(const GemmGroupArgs ga) {
-    constexpr int BM = 64, BN = 128, BK = 16;
-    constexpr int A_SZ = BM * (BK + 1), B_SZ = BN * (BK + 1);
-    constexpr int A_LD = BM * BK / 1024, B_LD = BN * BK / 1024;
-    constexpr int NOPT = BM * BN / 1024, NWT = NOPT;
-    static_assert(A_LD == 1 && B_LD == 2, "");
-    __shared__ __attribute__((aligned(16))) float ops[2 * (A_SZ + B_SZ)];
-    __shared__ __attribute__((aligned(16))) float gt[BM * DW_PT];
-    __shared__ float red[4];
-    const AdamEpi& e = ga.adam;
-    const int G = ga.nblk;
-    if ((int)blockIdx.x >= G) {
-        const int sb = blockIdx.x - G, nch = e.small.n_chunks;
-        adam_chunk(e.small, sb % nch, sb / nch);
-        return;
-    }
-    const int T = ga.first[ga.ng];
-    const int xc = blockIdx.x & 7, nbx = G >> 3;
-    const int hi = (int)((long long)T * (xc + 1) >> 3);
-    int t = (int)((long long)T * xc >> 3) + (int)(blockIdx.x >> 3);
-    if (t >= hi) return;
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wi = (wave >> 1) * 32, wj = (wave & 1) * 64;
-    const int l32 = lane & 31, lh = lane >> 5;
-    const int gK = ga.g[0].K;  // one K for the whole group
-    const int mode = e.mode;    // timing probes (FQLPOP_DW_MODE): 1 = no optimiser work, 2 = one k-slice
-    const int nk = mode == 2 ? 1 : (gK + BK - 1) / BK;
-    // unit schedule inside the k-loop of the next tile: optimiser unit u's loads at
-    // iteration u, its math at u + DWD; W^T unit w at NOPT + DWD + w; the rest after the loop
-    const bool inloop = nk >= NOPT + DWD;
-    const float lr = e.lr, tau = e.tau;
-
-    DwTile cur = dw_decode(ga, t);
-    float4 ra[A_LD], rb[B_LD];
-    {
-        const GemmArgs& g = ga.g[cur.gi];
-        const rsrc_t rA = make_rsrc(at(g.A, cur.slot, cur.y), (long long)(g.M - 1) * g.lda + g.K);
-        const rsrc_t rB = make_rsrc(at(g.B, cur.slot, cur.y), (long long)(g.N - 1) * g.ldb + g.K);
-        ra[0] = stage_load<BM, BK, true>(rA, g.lda, 0, cur.i0, 0);
-        rb[0] = stage_load<BN, BK, true>(rB, g.ldb, 0, cur.j0, 0);
-        rb[1] = stage_load<BN, BK, true>(rB, g.ldb, 1, cur.j0, 0);
-    }
-    stage_store<BM, BK, true>(ops, 0, ra[0]);
-    stage_store<BN, BK, true>(ops + A_SZ, 0, rb[0]);
-    stage_store<BN, BK, true>(ops + A_SZ, 1, rb[1]);
-    __syncthreads();
-
-    bool have_prev = false;
-    DwOpt pv{};
-    DwOptRegs oq[DWD + 1] = {};  // oq[0]: the unit computed this iteration, oq[DWD]: loaded now
-    float mx = -INFINITY, mn = INFINITY, ss = 0.f;
-    int it = 0;  // running k-iteration count: operand buffer parity across tiles
-    for (;;) {
-        const int tn = t + nbx;
-        const bool has_next = tn < hi;
-        const DwTile nx = has_next ? dw_decode(ga, tn) : cur;
-        const GemmArgs& gc = ga.g[cur.gi];
-        const GemmArgs& gn = ga.g[nx.gi];
-        const float* pA = at(gc.A, cur.slot, cur.y);
-        const float* pB = at(gc.B, cur.slot, cur.y);
-        const long long nA = (long long)(gc.M - 1) * gc.lda + gc.K, nB = (long long)(gc.N - 1) * gc.ldb + gc.K;
-        const float* qA = at(gn.A, nx.slot, nx.y);
-        const float* qB = at(gn.B, nx.slot, nx.y);
-        const long long mA = (long long)(gn.M - 1) * gn.lda + gn.K, mB = (long long)(gn.N - 1) * gn.ldb + gn.K;
-        const int clda = gc.lda, cldb = gc.ldb, nlda = gn.lda, nldb = gn.ldb;
-
-        f32x16 acc[2];
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-
-        for (int kt = 0; kt < nk; ++kt, ++it) {
-            const bool last = kt + 1 == nk;
-            // operand prefetch: slice kt+1 of this tile, or the next tile's first slice
-            // (the block's last tile re-reads its own first slice: no branch)
-            {
-                const rsrc_t xa = last ? make_rsrc(qA, mA) : make_rsrc(pA, nA);
-                const rsrc_t xb = last ? make_rsrc(qB, mB) : make_rsrc(pB, nB);
-                const int la = last ? nlda : clda, lb = last ? nldb : cldb;
-                const int ia = last ? nx.i0 : cur.i0, jb = last ? nx.j0 : cur.j0;
-                const int k0 = last ? 0 : (kt + 1) * BK;
-                ra[0] = stage_load<BM, BK, true>(xa, la, 0, ia, k0);
-                rb[0] = stage_load<BN, BK, true>(xb, lb, 0, jb, k0);
-                rb[1] = stage_load<BN, BK, true>(xb, lb, 1, jb, k0);
-            }
-            if (inloop && have_prev && kt < NOPT && mode != 1) dw_opt_load(oq[DWD], pv, kt);
-            __builtin_amdgcn_sched_barrier(0);
-            const float* Ac = ops + (it & 1) * (A_SZ + B_SZ);
-            const float* Bc = Ac + A_SZ;
-            float av[BK / 2], bv[BK / 2][2];
-#pragma unroll
-            for (int kk = 0; kk < BK / 2; ++kk) {
-                const int rr = 2 * kk + lh;
-                av[kk] = Ac[(wi + l32) * (BK + 1) + rr];
-#pragma unroll
-                for (int b = 0; b < 2; ++b) bv[kk][b] = Bc[(wj + b * 32 + l32) * (BK + 1) + rr];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int kk = 0; kk < BK / 2; ++kk)
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-                    acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk][b], acc[b], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (inloop && have_prev && mode != 1) {
-                if (kt >= DWD && kt < NOPT + DWD) dw_opt_compute(oq[0], pv, kt - DWD, gt, lr, tau, mx, mn, ss);
-                else if (kt >= NOPT + DWD && kt < NOPT + DWD + NWT && pv.hasWT) dw_wt_unit(pv, kt - NOPT - DWD, gt);
-            }
-            float* nb = ops + ((it + 1) & 1) * (A_SZ + B_SZ);
-            stage_store<BM, BK, true>(nb, 0, ra[0]);
-            stage_store<BN, BK, true>(nb + A_SZ, 0, rb[0]);
-            stage_store<BN, BK, true>(nb + A_SZ, 1, rb[1]);
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < DWD; ++q) oq[q] = oq[q + 1];
-        }
-
-        if (have_prev && mode != 1) {
-            if (!inloop) {
-                dw_drain(pv, gt, lr, tau, mx, mn, ss);
-            } else if (pv.hasWT) {
-                for (int w = max(0, nk - NOPT - DWD); w < NWT; ++w) dw_wt_unit(pv, w, gt);
-            }
-            dw_finish(pv, e.stats, mx, mn, ss, red);  // (its barriers retire every read of gt)
-        }
-        // this tile's gradient into the LDS image: row i = (r&3) + 8(r>>2) + 4 lh of a 32x32 tile
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                gt[(wi + (r & 3) + 8 * (r >> 2) + 4 * lh) * DW_PT + wj + b * 32 + l32] = acc[b][r];
-        __syncthreads();
-        pv = dw_opt_ctx(ga, cur);
-        have_prev = true;
-        mx = -INFINITY;
-        mn = INFINITY;
-        ss = 0.f;
-        if (!has_next) break;
-        cur = nx;
-        t = tn;
-    }
-    if (mode != 1) {
-        dw_drain(pv, gt, lr, tau, mx, mn, ss);
-        dw_finish(pv, e.stats, mx, mn, ss, red);
-    }
-}
-
-void launch_dwopt(const GemmArgs* gs, int ng, hipStream_t s, const AdamEpi& adam, int tpb, int n_cu) {
-    GemmGroupArgs ga{};
-    int tot = 0;
-    for (int i = 0; i < ng; ++i) {
-        ga.g[i] = gs[i];
-        ga.first[i] = tot;
-        tot += gemm_group_tiles(2, gs[i].M, gs[i].N) * gs[i].ny * gs[i].nz;
-    }
-    ga.first[ng] = tot;
-    ga.ng = ng;
-    ga.adam = adam;
-    const int per_xcd = (tot + 7) / 8;
-    const int cap = std::max(1, 2 * n_cu / 8);  // 2 blocks per CU
-    // tpb 0: every block slot of the chip (2 per CU), tile counts differing by at most one
-    const int nbx = std::max(1, std::min(cap, tpb > 0 ? (per_xcd + tpb - 1) / tpb : per_xcd));
-    ga.nblk = 8 * nbx;
-    static const int dwd = [] { const char* v = std::getenv("FQLPOP_DWOPT_DIST"); return v ? std::atoi(v) : 2; }();
-    const dim3 grid(ga.nblk + adam.small_blocks);
-    if (dwd <= 1) hipLaunchKernelGGL(dwopt_kernel<1>, grid, dim3(256), 0, s, ga);
-    else if (dwd == 2) hipLaunchKernelGGL(dwopt_kernel<2>, grid, dim3(256), 0, s, ga);
-    else hipLaunchKernelGGL(dwopt_kernel<3>, grid, dim3(256), 0, s, ga);
 }
 
 // ---------------------------------------------------------------------------

@@ -163,9 +163,6 @@ struct fqlpop {
     // W_l tiles, and the remaining (small-leaf) chunks the adam kernel runs
     bool fused_adam = false;
     bool cdw_sb = true;            // the critic's fused dW + optimiser on sB (beside the actor chain)
-    int dwopt_mask = 0;            // nets (bit ni) whose fused dW + optimiser runs pipelined (launch_dwopt)
-    int dwopt_tpb[3] = {0, 0, 0};  // its tiles per block (0: 2 blocks per CU)
-    int n_cu = 256;
     int w_stat_base[3][EF_MAX_LAYERS] = {};
     int* res_ids = nullptr;
     int res_base[3] = {0, 0, 0}, res_n[3] = {0, 0, 0};
@@ -714,9 +711,7 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         }
         ae.small = adam_args(c, ni);
         ae.small_blocks = ae.small.n_chunks * c.nz;
-        if ((h->dwopt_mask & (1 << ni)) && (dw_tile(N) & 3) == 2)  // (its stats chunks: 64 x 128 tiles)
-            launch_dwopt(gs.data(), (int)gs.size(), sw, ae, h->dwopt_tpb[ni], h->n_cu);
-        else launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw, &ae);
+        launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw, &ae);
     } else if (N.L <= GEMM_GROUP_MAX && N.H % 128 == 0) {
         launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw);
     } else {
@@ -1372,18 +1367,6 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             const char* fa = std::getenv("FQLPOP_FUSED_ADAM");
             h->fused_adam = h->stream_bwd && H % 128 == 0 && L <= GEMM_GROUP_MAX && h->critic.off == 0 &&
                             !(fa && std::atoi(fa) == 0);
-            // the pipelined form (optimiser of tile n inside the k-loop of tile n+1):
-            // FQLPOP_DWOPT = bit mask of nets (1 critic, 2 bc, 4 os), FQLPOP_DWOPT_TPB_{C,B,O}
-            const char* dp = std::getenv("FQLPOP_DWOPT");
-            h->dwopt_mask = h->fused_adam && dp ? std::atoi(dp) : 0;
-            const char* tn[3] = {"FQLPOP_DWOPT_TPB_C", "FQLPOP_DWOPT_TPB_B", "FQLPOP_DWOPT_TPB_O"};
-            for (int i = 0; i < 3; ++i) {
-                const char* v = std::getenv(tn[i]);
-                h->dwopt_tpb[i] = v ? std::atoi(v) : 0;
-            }
-            int ncu = 0;
-            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) == hipSuccess && ncu > 0)
-                h->n_cu = ncu;
         }
         if (h->euler_fused) {  // dominant kernel: one persistent Euler launch per step
             h->probe_pairs = 1;
