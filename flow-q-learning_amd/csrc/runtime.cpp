@@ -1185,6 +1185,7 @@ void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         }
         HIPCHK(hipStreamEndCapture(h->sM, &graph));
         HIPCHK(hipGraphInstantiate(&gr.exec, graph, nullptr, nullptr, 0));
+        HIPCHK(hipGraphUpload(gr.exec, h->sM));  // (else the first launch uploads it)
         HIPCHK(hipGraphDestroy(graph));
         gr.nz = h->nz;
     }

@@ -1,0 +1,54 @@
+"""Step rate right after setup, in chunks (developer tool, on the GPU box):
+
+  python flow-q-learning_amd/csrc/tools/step_ramp.py [chunk] [n_chunks] [idle_s]
+
+Builds the bench population (cube, 16 members, 1M rows), runs 5 warmup steps, then
+times n_chunks back-to-back chunks of `chunk` steps (host-synchronised each), then
+idles idle_s seconds and times 3 more chunks.  Shows how long the step rate takes
+to reach its steady state (clocks, caches, first graph replays).
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", "..", ".."))
+sys.path.insert(0, os.path.join(ROOT, "flow-q-learning_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from fqlpop import Population, PopulationConfig  # noqa: E402
+
+
+def main():
+    chunk = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    n_chunks = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+    idle = float(sys.argv[3]) if len(sys.argv) > 3 else 1.0
+    torch.cuda.set_device(0)
+    wl = bench.WORKLOADS["cube"]
+    data = bench.synthetic_dataset(1_000_000, wl["obs_dim"], wl["action_dim"])
+    alphas, seeds = bench.population_values(16)
+    pop = Population(PopulationConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"],
+                                      batch_size=wl["batch_size"]), alphas, seeds, device=0)
+    pop.set_dataset(data)
+    pop.step(5)
+    pop.sync()
+
+    def timed(tag):
+        t0 = time.perf_counter()
+        pop.step(chunk)
+        pop.sync()
+        el = time.perf_counter() - t0
+        print(f"{tag} {chunk} steps: {1e3 * el / chunk:.4f} ms/step  {16 * chunk / el:.1f} member-steps/s", flush=True)
+
+    for i in range(n_chunks):
+        timed(f"chunk {i:2d}")
+    time.sleep(idle)
+    for i in range(3):
+        timed(f"after {idle:.1f} s idle, chunk {i}")
+    pop.close()
+
+
+if __name__ == "__main__":
+    main()
