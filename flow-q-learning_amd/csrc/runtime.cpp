@@ -603,6 +603,8 @@ AdamArgs adam_args(const Ctx& c, int ni);
 // partial reduction (bias / LN / head-kernel grads) and the dW_l GEMMs.
 // Activations are read at column offset `coff` (ld `ld`), du_l written with
 // ld `ld_d`; M columns are back-propagated, the first Mg feed the grads.
+int skip_mask();
+
 void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_o, TRef X0, int ld,
                     long long coff, int M, int Mg, const std::vector<float*>& U, const std::vector<float*>& G,
                     long long act_sy, const std::vector<float*>* MU, const std::vector<float*>* RS, long long st_sy,
@@ -646,7 +648,7 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         a.da = ig->da.p; a.da_ss = ig->da.ss; a.da_sy = (long long)ig->A * ig->M;
         a.ld_da = ig->M; a.D0 = ig->D; a.na = ig->A;
     }
-    launch_stream_bwd(N.ln, a, s);
+    if (!(skip_mask() & (&N == &h->critic ? 32 : &N == &h->bc ? 64 : 128))) launch_stream_bwd(N.ln, a, s);
     hipEvent_t ev = nullptr;
     if (sw != s) {
         ev = next_event(h);
@@ -819,7 +821,18 @@ void stream_fwd(const Ctx& c, hipStream_t s, const NetLayout& N, const float* ar
     a.head = head;
     a.head.nout = N.out_dim;
     a.ny = N.E; a.nz = c.nz; a.slots = h->slots;
-    launch_stream_fwd(mode, N.ln, a, s);
+    const int sk = skip_mask();
+    const int bit = &N == &h->bc ? 16 : &N == &h->os ? 8 : arena == h->target ? 2 : 4;
+    if (!(sk & bit)) launch_stream_fwd(mode, N.ln, a, s);
+}
+
+// FQLPOP_SKIP (TIMING EXPERIMENT ONLY, results are garbage): bit mask of launches left
+// out of the step, to measure each one's marginal cost in the concurrent step:
+// 1 Euler flow, 2 target-critic fwd, 4 critic fwd, 8 one-step fwd, 16 BC fwd,
+// 32 critic bwd (dX chain), 64 BC bwd, 128 one-step bwd
+int skip_mask() {
+    static const int m = [] { const char* v = std::getenv("FQLPOP_SKIP"); return v ? std::atoi(v) : 0; }();
+    return m;
 }
 
 // Arguments of the persistent Euler-flow launch: steps 1..S-1 from eu_in (the
@@ -949,7 +962,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             EulerArgs ea = euler_args(h, c.nz);
             if (h->probe_set >= 0 && h->probe_idx < h->probe_pairs)
                 ea.probe = h->probe_slots + 2 * h->probe_blocks * ((long long)h->probe_set * h->probe_pairs + h->probe_idx++);
-            launch_euler_flow(ea, sF);
+            if (!(skip_mask() & 1)) launch_euler_flow(ea, sF);
         }
         for (int i = 1; !h->euler_fused && i < S + (S == 1 ? 1 : 0); ++i) {
             // S == 1: one zero-cost pass that only clips (not used by the configs here)
