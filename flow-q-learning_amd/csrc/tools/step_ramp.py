@@ -1,6 +1,6 @@
 """Step rate right after setup, in chunks (developer tool, on the GPU box):
 
-  python flow-q-learning_amd/csrc/tools/step_ramp.py [chunk] [n_chunks] [idle_s]
+  python flow-q-learning_amd/csrc/tools/step_ramp.py [chunk] [n_chunks] [idle_s] [preheat_ms]
 
 Builds the bench population (cube, 16 members, 1M rows), runs 5 warmup steps, then
 times n_chunks back-to-back chunks of `chunk` steps (host-synchronised each), then
@@ -25,6 +25,7 @@ def main():
     chunk = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     n_chunks = int(sys.argv[2]) if len(sys.argv) > 2 else 12
     idle = float(sys.argv[3]) if len(sys.argv) > 3 else 1.0
+    preheat_ms = float(sys.argv[4]) if len(sys.argv) > 4 else 0.0
     torch.cuda.set_device(0)
     wl = bench.WORKLOADS["cube"]
     data = bench.synthetic_dataset(1_000_000, wl["obs_dim"], wl["action_dim"])
@@ -32,6 +33,9 @@ def main():
     pop = Population(PopulationConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"],
                                       batch_size=wl["batch_size"]), alphas, seeds, device=0)
     pop.set_dataset(data)
+    if preheat_ms > 0:  # as bench.py --preheat-ms
+        us, _ = pop.time_dominant_kernel(1)
+        pop.time_dominant_kernel(max(1, int(preheat_ms * 1e3 / us)))
     pop.step(5)
     pop.sync()
 
