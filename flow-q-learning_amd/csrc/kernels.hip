@@ -273,6 +273,20 @@ DEV void st4(float* p, float4 v, int nt) {
     else *reinterpret_cast<float4*>(p) = v;
 }
 
+// float4 buffer load / store with a cache policy: nt = non-temporal (a streamed optimiser
+// operand read and written once per step need not displace the weights the streamed
+// kernels re-read from L2 / MALL)
+constexpr int BUF_AUX_NT = 2;
+DEV float4 bload4_aux(rsrc_t r, int off_b, int nt) {
+    return __builtin_bit_cast(float4, nt ? __builtin_amdgcn_raw_buffer_load_b128(r, off_b, 0, BUF_AUX_NT)
+                                         : __builtin_amdgcn_raw_buffer_load_b128(r, off_b, 0, 0));
+}
+DEV void bstore4_aux(rsrc_t r, float4 v, int off_b, int nt) {
+    const auto w = __builtin_bit_cast(__attribute__((ext_vector_type(4))) int, v);
+    if (nt) __builtin_amdgcn_raw_buffer_store_b128(w, r, off_b, 0, BUF_AUX_NT);
+    else __builtin_amdgcn_raw_buffer_store_b128(w, r, off_b, 0, 0);
+}
+
 template <int BM, int BN, bool DUAL>
 DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc)[BM / 64][BN / 64],
                        f32x16 (&acc2)[BM / 64][BN / 64], int slot, int y, int tile, int per, int i0, int j0,
@@ -281,6 +295,43 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
     constexpr int PT = BN + 1;  // LDS row pitch (odd: the transposed read of pass 2 spreads over banks)
     // (the launching kernel sizes smem for the gradient tile: group_smem_floats)
     const int gM = g.M, ldc = g.ldc, tid = threadIdx.x;
+    const long long pb = (long long)slot * e.P + e.w_off[gi] + (long long)y * e.ens;
+    // the leaf as buffer resources: rows past M (the first layer's last tile) read 0 and
+    // their stores drop, so no access needs a row guard (a guarded load is a branch + a
+    // vmcnt(0) wait)
+    const long long nleaf = (long long)gM * ldc;
+    const rsrc_t rP = make_rsrc(e.p_in + pb, nleaf), rPo = make_rsrc(e.p_out + pb, nleaf);
+    const rsrc_t rM = make_rsrc(e.m + pb, nleaf), rV = make_rsrc(e.v + pb, nleaf);
+    // the target arena mirrors the critic block, which sits at arena offset 0
+    const bool hasT = e.target != nullptr;
+    const rsrc_t rT = make_rsrc(hasT ? e.target + (long long)slot * e.PT + e.w_off[gi] + (long long)y * e.ens
+                                     : e.m + pb, nleaf);
+    const float t = (float)(e.count[slot] + 1);
+    const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
+    const float rbc1 = 1.0f / bc1, rbc2 = 1.0f / bc2;
+    const float lr = e.lr, tau = e.tau;
+    float mx = -INFINITY, mn = INFINITY, ss = 0.f;
+    const int rows = min(BM, gM - i0);
+    const bool run = e.mode != 1;  // mode 1: timing probe only (no optimiser traffic)
+    // pass 1: thread -> 4 consecutive columns of a row, U rows per batch, two batches in
+    // flight (p, m, v, target do not depend on the gradient: batch 0 is issued before the
+    // gradient tile is staged); m, v and the target stream non-temporally
+    constexpr int TPR = BN / 4, RPI = 256 / TPR, U = 2, NB = BM / (RPI * U);
+    static_assert(NB * RPI * U == BM && NB >= 2, "");
+    const int cj = (tid % TPR) * 4, ri = tid / TPR;
+    float4 p4[2][U], m4[2][U], v4[2][U], t4[2][U];
+    auto issue = [&](int bi, int q) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = bi * RPI * U + u * RPI + ri;
+            const int off = ((i0 + i) * ldc + j0 + cj) * 4;
+            p4[q][u] = bload4_aux(rP, off, 0);
+            m4[q][u] = bload4_aux(rM, off, 1);
+            v4[q][u] = bload4_aux(rV, off, 1);
+            t4[q][u] = hasT ? bload4_aux(rT, off, 1) : float4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    if (run) issue(0, 0);
     __syncthreads();  // every wave is done with the operand buffers
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -292,47 +343,21 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
                 smem[(wi + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * PT + wj + b * 32 + l32] = acc[a][b][r];
         }
     __syncthreads();
-
-    const long long pb = (long long)slot * e.P + e.w_off[gi] + (long long)y * e.ens;
-    const float* __restrict__ Pi = e.p_in + pb;
-    float* __restrict__ Po = e.p_out + pb;
-    float* __restrict__ Mm = e.m + pb;
-    float* __restrict__ Vv = e.v + pb;
-    // the target arena mirrors the critic block, which sits at arena offset 0
-    float* __restrict__ Tt = e.target ? e.target + (long long)slot * e.PT + e.w_off[gi] + (long long)y * e.ens : nullptr;
-    const float t = (float)(e.count[slot] + 1);
-    const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
-    const float rbc1 = 1.0f / bc1, rbc2 = 1.0f / bc2;
-    const float lr = e.lr, tau = e.tau;
-    const int nt = e.nt;
-    float mx = -INFINITY, mn = INFINITY, ss = 0.f;
-    const int rows = e.mode == 1 ? 0 : min(BM, gM - i0);  // mode 1: timing probe only (no optimiser traffic)
-    // pass 1: thread -> 4 consecutive columns of a row; U iterations in flight
-    constexpr int TPR = BN / 4, RPI = 256 / TPR, U = 4;  // threads per row, rows per iteration
-    const int cj = (tid % TPR) * 4, ri = tid / TPR;
-    for (int r0 = 0; r0 < BM; r0 += RPI * U) {
-        float4 p4[U], m4[U], v4[U], t4[U];
+    if (run) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = r0 + u * RPI + ri;
-            if (i < rows) {
-                const long long o = (long long)(i0 + i) * ldc + j0 + cj;
-                p4[u] = ld4(Pi + o, nt & 4);
-                m4[u] = ld4(Mm + o, nt & 1);
-                v4[u] = ld4(Vv + o, nt & 1);
-                if (Tt) t4[u] = ld4(Tt + o, nt & 2);
-            }
-        }
+        for (int bi = 0; bi < NB; ++bi) {
+            const int q = bi & 1;
+            if (bi + 1 < NB) issue(bi + 1, q ^ 1);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = r0 + u * RPI + ri;
-            if (i < rows) {
-                const long long o = (long long)(i0 + i) * ldc + j0 + cj;
+            for (int u = 0; u < U; ++u) {
+                const int i = bi * RPI * U + u * RPI + ri;
+                const int off = ((i0 + i) * ldc + j0 + cj) * 4;
+                const bool live = i < rows;
                 float* gs = smem + i * PT + cj;
-                float pp[4] = {p4[u].x, p4[u].y, p4[u].z, p4[u].w};
-                float mm[4] = {m4[u].x, m4[u].y, m4[u].z, m4[u].w};
-                float vv[4] = {v4[u].x, v4[u].y, v4[u].z, v4[u].w};
-                float tt[4] = {t4[u].x, t4[u].y, t4[u].z, t4[u].w};
+                float pp[4] = {p4[q][u].x, p4[q][u].y, p4[q][u].z, p4[q][u].w};
+                float mm[4] = {m4[q][u].x, m4[q][u].y, m4[q][u].z, m4[q][u].w};
+                float vv[4] = {v4[q][u].x, v4[q][u].y, v4[q][u].z, v4[q][u].w};
+                float tt[4] = {t4[q][u].x, t4[q][u].y, t4[q][u].z, t4[q][u].w};
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     const float gr = gs[c];
@@ -344,14 +369,14 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
                     tt[c] = tau * pp[c] + (1.0f - tau) * tt[c];
                     pp[c] = pp[c] + (-lr) * (mh * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vh) + 1e-8f));
                     gs[c] = pp[c];
-                    mx = fmaxf(mx, gr);
-                    mn = fminf(mn, gr);
-                    ss += gr * gr;
+                    mx = live ? fmaxf(mx, gr) : mx;
+                    mn = live ? fminf(mn, gr) : mn;
+                    ss = live ? ss + gr * gr : ss;
                 }
-                st4(Po + o, float4{pp[0], pp[1], pp[2], pp[3]}, nt & 8);
-                st4(Mm + o, float4{mm[0], mm[1], mm[2], mm[3]}, nt & 1);
-                st4(Vv + o, float4{vv[0], vv[1], vv[2], vv[3]}, nt & 1);
-                if (Tt) st4(Tt + o, float4{tt[0], tt[1], tt[2], tt[3]}, nt & 2);
+                bstore4_aux(rPo, float4{pp[0], pp[1], pp[2], pp[3]}, off, 0);
+                bstore4_aux(rM, float4{mm[0], mm[1], mm[2], mm[3]}, off, 1);
+                bstore4_aux(rV, float4{vv[0], vv[1], vv[2], vv[3]}, off, 1);
+                if (hasT) bstore4_aux(rT, float4{tt[0], tt[1], tt[2], tt[3]}, off, 1);
             }
         }
     }
@@ -366,6 +391,7 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
         st[2] = ss;
     }
     // pass 2 (hidden layers: M = H, full tiles): W^T[j][i0 .. i0+BM) as float4 runs along i
+    const int nt = e.nt;
     if (e.wt_off[gi] >= 0 && e.mode != 1) {
         float* __restrict__ WT = e.wt_out + (long long)slot * e.PTT + e.wt_off[gi] + (long long)y * e.wt_sy;
         constexpr int TPC = BM / 4;  // threads per W^T row segment
