@@ -58,6 +58,28 @@ DEV float wave_min(float v) {
     return v;
 }
 
+// Sum over the 4 lanes l, l^16, l^32, l^48 (the lk index of the streamed kernels' lane
+// layout), every lane getting the sum: v_permlane16_swap / v_permlane32_swap (VALU, no
+// LDS traffic and no per-lane ds_bpermute address to keep live; __shfl_xor's addresses
+// were the spilled registers of the LN backward).  The same additions as
+// v += shfl_xor(v, 16); v += shfl_xor(v, 32) (fp add is commutative): bit-identical.
+// Inline asm: this compiler folds the two results of __builtin_amdgcn_permlane16_swap
+// into one when both inputs are the same value.  The s_nop covers the VALU-write ->
+// permlane-read hazard.
+// an opaque copy of v (the compiler cannot hoist what is computed from it)
+DEV int opq(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+DEV float lk_sum(float v) {
+    float a = v, b = v;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    float s = a + b, c = s;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(s), "+v"(c));
+    return s + c;
+}
+
 // Block-wide reductions for 256-thread blocks; `red` needs 4 floats.
 DEV float block_sum(float v, float* red) {
     v = wave_sum(v);
@@ -1325,10 +1347,8 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
                     s1 += v[r][c];
                     s2 += v[r][c] * v[r][c];
                 }
-            s1 += __shfl_xor(s1, 16, 64);
-            s2 += __shfl_xor(s2, 16, 64);
-            s1 += __shfl_xor(s1, 32, 64);
-            s2 += __shfl_xor(s2, 32, 64);
+            s1 = lk_sum(s1);
+            s2 = lk_sum(s2);
             if (lk == 0) {
                 lnred[0][w][li] = s1;
                 lnred[1][w][li] = s2;
@@ -1672,11 +1692,6 @@ DEV float row16_sum(float v) {
     return v;
 }
 // Sum over lk (lanes li, li+16, li+32, li+48).
-DEV float lk_sum(float v) {
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    return v;
-}
 
 bool stream_bwd_supported(int H, int L, int nout, int M, int Mg) {
     return H == EF_H && L >= 1 && L <= EF_MAX_LAYERS && nout >= 1 && nout <= 8 && M % EF_NC == 0 &&
@@ -1777,23 +1792,27 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
     // epilogue inputs of layer l (u, LN stats, LN scale), loaded one layer ahead
     // so that their latency hides under the previous dX product
     float u[4][4], gth = 0.f, mu = 0.f, rs = 0.f;  // gth: LN scale of feature tid (staged through LDS)
-    auto load_epi = [&](int l) {
+    // (lane indices as arguments: inside the layer loop they come from an opaque copy of
+    // tid, so that per-lane addresses are recomputed where they are used instead of
+    // being hoisted out of the loop and spilled: every spill reload was a vmcnt(0) that
+    // also waited for the ring refills and the du stores in flight)
+    auto load_epi = [&](int l, int tid_, int li_, int lk_) {
         const rsrc_t rU = make_rsrc(g.U[l] + so, (long long)H * g.ld_s);
-        const int vo = ((64 * w + 16 * lk) * g.ld_s + li) * 4;
+        const int vo = ((64 * w + 16 * lk_) * g.ld_s + li_) * 4;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int c = 0; c < 4; ++c) u[r][c] = bload1(rU, vo, (4 * r + c) * g.ld_s * 4);
         if constexpr (LN) {
-            mu = bload1(make_rsrc(g.MU[l] + sto, NC), li * 4, 0);
-            rs = bload1(make_rsrc(g.RS[l] + sto, NC), li * 4, 0);
-            gth = bload1(rPe, tid * 4, (int)g.g_off[l] * 4);
+            mu = bload1(make_rsrc(g.MU[l] + sto, NC), li_ * 4, 0);
+            rs = bload1(make_rsrc(g.RS[l] + sto, NC), li_ * 4, 0);
+            gth = bload1(rPe, tid_ * 4, (int)g.g_off[l] * 4);
         }
     };
-    load_epi(L - 1);
+    load_epi(L - 1, tid, li, lk);
     // parameter-grad partials, thread = feature: sums over the block's 16 columns of an LDS image
-    auto row_sum = [&](const float* a) {
-        const float4* row = reinterpret_cast<const float4*>(&a[tid * NC]);
+    auto row_sum = [&](const float* a, int tid_) {
+        const float4* row = reinterpret_cast<const float4*>(&a[tid_ * NC]);
         float sv = 0.f;
 #pragma unroll
         for (int q = 0; q < NC / 4; ++q) {
@@ -1802,15 +1821,17 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         }
         return sv;
     };
-    // this lane's element (feature 64w + 16lk, column li) of an [H][NC] LDS image; element
-    // (r, c) is at + (4r + c) * NC (ds_write immediate offsets, one address VGPR)
-    const int lofs = (64 * w + 16 * lk) * NC + li;
-    float* const slab_l = slab + lofs;
-    float* const scr_l = scr + lofs;
     for (int l = L - 1; l >= 0; --l) {
+        // (the critic's LN variant only: the actor backward has no spills, and the opaque
+        // lane indices slowed its in-step launch 2x beside the flow)
+        const int tid_l = LN ? opq(tid) : tid, li_l = tid_l & 15, lk_l = (tid_l >> 4) & 3;
+        // this lane's element (feature 64w + 16lk, column li_l) of an [H][NC] LDS image; element
+        // (r, c) is at + (4r + c) * NC (ds_write immediate offsets, one address VGPR)
+        float* const slab_l = slab + (64 * w + 16 * lk_l) * NC + li_l;
+        float* const scr_l = scr + (64 * w + 16 * lk_l) * NC + li_l;
         // ---- du_l from dh = dL/dG_l (GELU', LayerNorm backward), in place in dh ----
         if constexpr (LN) {
-            gams[tid] = gth;
+            gams[tid_l] = gth;
             // pass 1: xhat, GELU' (kept in u); dh and dh * xhat to LDS (LN bias / scale grads;
             // the slab is free: the previous product is done with it)
             float xh[4][4];
@@ -1830,7 +1851,7 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
             float s1 = 0.f, s2 = 0.f;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float4 g4 = *reinterpret_cast<const float4*>(&gams[64 * w + 16 * lk + 4 * r]);
+                const float4 g4 = *reinterpret_cast<const float4*>(&gams[64 * w + 16 * lk_l + 4 * r]);
                 const float gr[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
@@ -1841,20 +1862,20 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
             }
             s1 = lk_sum(s1);
             s2 = lk_sum(s2);
-            if (lk == 0) {
-                colred[0][w][li] = s1;
-                colred[1][w][li] = s2;
+            if (lk_l == 0) {
+                colred[0][w][li_l] = s1;
+                colred[1][w][li_l] = s2;
             }
             if (gp) {
-                bstore1(rPart, row_sum(scr), tid * 4, (2 * L + l) * H * 4);   // LN bias: sum dh
-                bstore1(rPart, row_sum(slab), tid * 4, (L + l) * H * 4);      // LN scale: sum dh * xhat
+                bstore1(rPart, row_sum(scr, tid_l), tid_l * 4, (2 * L + l) * H * 4);   // LN bias: sum dh
+                bstore1(rPart, row_sum(slab, tid_l), tid_l * 4, (L + l) * H * 4);      // LN scale: sum dh * xhat
             }
             __syncthreads();  // colred visible; scr, slab free
             float c1 = 0.f, c2 = 0.f;
 #pragma unroll
             for (int q8 = 0; q8 < EF_NW; ++q8) {
-                c1 += colred[0][q8][li];
-                c2 += colred[1][q8][li];
+                c1 += colred[0][q8][li_l];
+                c2 += colred[1][q8][li_l];
             }
             c1 = c1 / (float)H;
             c2 = c2 / (float)H;
@@ -1873,7 +1894,7 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
             // du_l is the dW GEMMs' operand (grad columns) or input_grad_kernel's; the dQ/da
             // columns of a fused backward need it only in LDS
             const rsrc_t rD = make_rsrc(g.DU[l] + dso, (long long)H * g.ld_d);
-            const int vo = ((64 * w + 16 * lk) * g.ld_d + li) * 4;
+            const int vo = ((64 * w + 16 * lk_l) * g.ld_d + li_l) * 4;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -1888,11 +1909,11 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
                 for (int c = 0; c < 4; ++c) slab_l[(4 * r + c) * NC] = dh[r][c];
         }
         __syncthreads();
-        if (gp) bstore1(rPart, row_sum(slab), tid * 4, l * H * 4);  // bias: sum du
+        if (gp) bstore1(rPart, row_sum(slab, tid_l), tid_l * 4, l * H * 4);  // bias: sum du
         if (l == 0 && g.da != nullptr && !gp) {
             // dQ/da for the actor's Q-loss columns (replaces input_grad_kernel): output (j, col)
             // = thread & 127, feature quarter = thread >> 7, then a fixed-order fold in scr
-            const int o = tid & 127, q = tid >> 7, j = o >> 4, col = o & 15;
+            const int o = tid_l & 127, q = tid_l >> 7, j = o >> 4, col = o & 15;
             float s = 0.f;
             if (j < g.na) {
                 const float* __restrict__ wr = P + g.w_off[0] + (long long)(g.D0 + j) * H;
@@ -1901,19 +1922,19 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
             }
             scr[q * 128 + o] = s;
             __syncthreads();
-            if (tid < g.na * NC)
-                g.da[(long long)slot * g.da_ss + (long long)y * g.da_sy + (long long)(tid >> 4) * g.ld_da +
-                     (c0 - g.Mg) + (tid & 15)] = scr[tid] + scr[128 + tid] + scr[256 + tid] + scr[384 + tid];
+            if (tid_l < g.na * NC)
+                g.da[(long long)slot * g.da_ss + (long long)y * g.da_sy + (long long)(tid_l >> 4) * g.ld_da +
+                     (c0 - g.Mg) + (tid_l & 15)] = scr[tid_l] + scr[128 + tid_l] + scr[256 + tid_l] + scr[384 + tid_l];
         }
         if (l == 0) break;
 
         // ---- dh_{l-1} = W_l du_l = (W_l^T)^T du_l: the forward k-loop on W_l^T ----
-        load_epi(l - 1);
+        load_epi(l - 1, tid_l, li_l, lk_l);
         f32x4 acc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int wn = (int)g.wt_off[l >= 2 ? l - 1 : l];  // next product's W^T (l-1 >= 1), else a harmless re-load
-        ef_kloop<PF>(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lo, lk, li);
+        ef_kloop<PF>(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lk_l * H + 64 * w + 4 * li_l, lk_l, li_l);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
