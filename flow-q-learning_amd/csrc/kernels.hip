@@ -72,6 +72,14 @@ DEV int opq(int v) {
     return v;
 }
 
+// the lane id (0..63) from v_mbcnt, in volatile asm: recomputed where it is used, never
+// hoisted (and so never spilled) by the compiler
+DEV int lane_id_asm() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 DEV float lk_sum(float v) {
     float a = v, b = v;
     asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
@@ -1746,14 +1754,6 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         for (int q = 0; q < 8; ++q)
             if (tid + q * NT < H * nout) scr[tid + q * NT] = hv[q];
     }
-    // W^T ring: the first PF k-steps of the first dX product (W_{L-1}^T)
-    const int lo = lk * H + 64 * w + 4 * li;
-    float4 ring[PF];
-    {
-        const int wf = L > 1 ? (int)g.wt_off[L - 1] : 0;
-#pragma unroll
-        for (int p = 0; p < PF; ++p) ring[p] = bload4(rT, wf + 4 * p * H + lo);
-    }
     __syncthreads();
 
     // head kernel grad partials (thread = feature): sum_col G_{L-1}[k][col] dout[j][col]
@@ -1810,6 +1810,17 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         }
     };
     load_epi(L - 1, tid, li, lk);
+    // W^T ring: the first PF k-steps of the first dX product (W_{L-1}^T), issued after the
+    // epilogue loads as in the layer loop, so that the loop head waits for the epilogue
+    // loads only (vmcnt(PF)) instead of for everything in flight (a vmcnt(0) that also
+    // waited for the ring refills of the next product, every layer)
+    const int lo = lk * H + 64 * w + 4 * li;
+    float4 ring[PF];
+    {
+        const int wf = L > 1 ? (int)g.wt_off[L - 1] : 0;
+#pragma unroll
+        for (int p = 0; p < PF; ++p) ring[p] = bload4(rT, wf + 4 * p * H + lo);
+    }
     // parameter-grad partials, thread = feature: sums over the block's 16 columns of an LDS image
     auto row_sum = [&](const float* a, int tid_) {
         const float4* row = reinterpret_cast<const float4*>(&a[tid_ * NC]);
@@ -1824,7 +1835,10 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
     for (int l = L - 1; l >= 0; --l) {
         // (the critic's LN variant only: the actor backward has no spills, and the opaque
         // lane indices slowed its in-step launch 2x beside the flow)
-        const int tid_l = LN ? opq(tid) : tid, li_l = tid_l & 15, lk_l = (tid_l >> 4) & 3;
+        // (the lane id from mbcnt, not from tid: a kept tid was itself spilled, and its reload
+        // at the loop head was a vmcnt(0))
+        const int lane_l = LN ? lane_id_asm() : lane;
+        const int tid_l = 64 * w + lane_l, li_l = lane_l & 15, lk_l = lane_l >> 4;
         // this lane's element (feature 64w + 16lk, column li_l) of an [H][NC] LDS image; element
         // (r, c) is at + (4r + c) * NC (ds_write immediate offsets, one address VGPR)
         float* const slab_l = slab + (64 * w + 16 * lk_l) * NC + li_l;
