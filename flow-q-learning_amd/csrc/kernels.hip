@@ -114,6 +114,18 @@ DEV float block_min(float v, float* red) {
     return fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
 }
 
+// Block-uniform values through readfirstlane (SGPRs): see gemm_body
+DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+DEV long long uni64(long long v) {
+    const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffffLL));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return ((long long)hi << 32) | (unsigned int)lo;
+}
+template <class T>
+DEV T* uniptr(T* p) {
+    return reinterpret_cast<T*>(uni64(reinterpret_cast<long long>(p)));
+}
+
 // Bijective XCD-aware remap: blocks b and b+8 share an XCD under round-robin
 // dispatch, so give each XCD a contiguous range of logical work ids (members'
 // tiles then share that XCD's L2 for their weight panel).  Speed only.
@@ -324,8 +336,8 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
     constexpr int TM = BM / 64, TN = BN / 64;
     constexpr int PT = BN + 1;  // LDS row pitch (odd: the transposed read of pass 2 spreads over banks)
     // (the launching kernel sizes smem for the gradient tile: group_smem_floats)
-    const int gM = g.M, ldc = g.ldc, tid = threadIdx.x;
-    const long long pb = (long long)slot * e.P + e.w_off[gi] + (long long)y * e.ens;
+    const int gM = uni(g.M), ldc = uni(g.ldc), tid = threadIdx.x;
+    const long long pb = uni64((long long)slot * e.P + e.w_off[gi] + (long long)y * e.ens);
     // the leaf as buffer resources: rows past M (the first layer's last tile) read 0 and
     // their stores drop, so no access needs a row guard (a guarded load is a branch + a
     // vmcnt(0) wait)
@@ -334,8 +346,8 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
     const rsrc_t rM = make_rsrc(e.m + pb, nleaf), rV = make_rsrc(e.v + pb, nleaf);
     // the target arena mirrors the critic block, which sits at arena offset 0
     const bool hasT = e.target != nullptr;
-    const rsrc_t rT = make_rsrc(hasT ? e.target + (long long)slot * e.PT + e.w_off[gi] + (long long)y * e.ens
-                                     : e.m + pb, nleaf);
+    const rsrc_t rT = make_rsrc(uniptr(hasT ? e.target + (long long)slot * e.PT + e.w_off[gi] + (long long)y * e.ens
+                                            : e.m + pb), nleaf);
     const float t = (float)(e.count[slot] + 1);
     const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
     const float rbc1 = 1.0f / bc1, rbc2 = 1.0f / bc2;
@@ -443,17 +455,21 @@ DEV void gemm_body(const GemmArgs& g, int w, float* smem, const AdamEpi* ae = nu
     constexpr int A_LD = BM * BK / 1024;  // float4 loads per thread
     constexpr int B_LD = BN * BK / 1024;
 
-    const int tiles_m = g.M / BM + (g.M % BM != 0), tiles_n = g.N / BN;  // host guarantees N % BN == 0
+    // (every block-level value through readfirstlane: in the grouped launch g is ga.g[gi]
+    // with a run-time gi, its fields come back in VGPRs, and buffer resources built from
+    // them were re-read through waterfall loops around every operand load of the k-loop)
+    const int gM = uni(g.M), gN = uni(g.N), gK = uni(g.K), lda = uni(g.lda), ldb = uni(g.ldb);
+    const int tiles_m = gM / BM + (gM % BM != 0), tiles_n = gN / BN;  // host guarantees N % BN == 0
     const int per = tiles_m * tiles_n;
     const int tile = w % per, yz = w / per;
-    const int y = yz % g.ny, z = yz / g.ny;
-    const int slot = g.slots[z];
+    const int gny = uni(g.ny);
+    const int y = yz % gny, z = yz / gny;
+    const int slot = uni(g.slots[z]);
     const int i0 = (tile / tiles_n) * BM, j0 = (tile % tiles_n) * BN;
-    const int gM = g.M, gN = g.N, gK = g.K, lda = g.lda, ldb = g.ldb;
 
     // valid extents (elements) of the two operands from their base
-    const rsrc_t rA = make_rsrc(at(g.A, slot, y), ARC ? (long long)(gM - 1) * lda + gK : (long long)(gK - 1) * lda + gM);
-    const rsrc_t rB = make_rsrc(at(g.B, slot, y), BRC ? (long long)(gN - 1) * ldb + gK : (long long)(gK - 1) * ldb + gN);
+    const rsrc_t rA = make_rsrc(uniptr(at(g.A, slot, y)), ARC ? (long long)(gM - 1) * lda + gK : (long long)(gK - 1) * lda + gM);
+    const rsrc_t rB = make_rsrc(uniptr(at(g.B, slot, y)), BRC ? (long long)(gN - 1) * ldb + gK : (long long)(gK - 1) * ldb + gN);
 
     float* As0 = smem;
     float* Bs0 = smem + A_SZ;
