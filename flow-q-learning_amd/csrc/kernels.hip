@@ -275,22 +275,37 @@ DEV float4 stage_load(rsrc_t X, int ld, int p, int i0, int k0) {
     }
 }
 
-template <int TILE, int BK, bool RC>
+// r-contiguous LDS image pitch: BK + 1 (conflict-free ds_read_b32 fragments), or BK + 4 with
+// the "k-blocked" fragment order (KB): lane half lh of a 32x32x2 MFMA reads k = 8 lh + kk
+// instead of 2 kk + lh, so its 8 k-values of a 16-wide slice are contiguous (two
+// ds_read_b128 instead of eight ds_read_b32) and the staging writes are float4 too; a
+// pitch of 20 floats keeps 16 consecutive lanes' b128 reads on distinct banks
+template <int BK, bool KB>
+constexpr int rc_pitch() { return KB ? BK + 4 : BK + 1; }
+template <int BM, int BN, int BK, bool ARC, bool BRC, int EPI>
+constexpr bool gemm_kb() { return ARC && BRC && BK == 16 && EPI == EPI_ADAM; }
+
+template <int TILE, int BK, bool RC, int PITCH = BK + 1>
 DEV void stage_store(float* __restrict__ S, int p, float4 v) {
     const int idx = threadIdx.x + 256 * p;
     if constexpr (RC) {
         const int row = idx / (BK / 4), c = (idx % (BK / 4)) * 4;
-        float* d = S + row * (BK + 1) + c;
-        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        float* d = S + row * PITCH + c;
+        if constexpr (PITCH % 4 == 0) {
+            *reinterpret_cast<float4*>(d) = v;
+        } else {
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
     } else {
         const int row = idx / (TILE / 4), c = (idx % (TILE / 4)) * 4;
         *reinterpret_cast<float4*>(S + row * TILE + c) = v;
     }
 }
 
-template <int BM, int BN, int BK, bool ARC, bool BRC>
+template <int BM, int BN, int BK, bool ARC, bool BRC, bool KB = false>
 constexpr int gemm_smem_floats() {
-    return 2 * ((ARC ? BM * (BK + 1) : BK * BM) + (BRC ? BN * (BK + 1) : BK * BN)) + BM;
+    constexpr int P = rc_pitch<BK, KB>();
+    return 2 * ((ARC ? BM * P : BK * BM) + (BRC ? BN * P : BK * BN)) + BM;
 }
 
 // Fused optimiser epilogue of a dW tile (AdamEpi in kernels.h).  The gradient
@@ -450,8 +465,10 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
 template <int BM, int BN, int BK, bool DUAL, bool ARC, bool BRC, int EPI>
 DEV void gemm_body(const GemmArgs& g, int w, float* smem, const AdamEpi* ae = nullptr, int gi = 0) {
     constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
-    constexpr int A_SZ = ARC ? BM * (BK + 1) : BK * BM;
-    constexpr int B_SZ = BRC ? BN * (BK + 1) : BK * BN;
+    constexpr bool KB = gemm_kb<BM, BN, BK, ARC, BRC, EPI>();
+    constexpr int RP = rc_pitch<BK, KB>();
+    constexpr int A_SZ = ARC ? BM * RP : BK * BM;
+    constexpr int B_SZ = BRC ? BN * RP : BK * BN;
     constexpr int A_LD = BM * BK / 1024;  // float4 loads per thread
     constexpr int B_LD = BN * BK / 1024;
 
@@ -508,9 +525,9 @@ DEV void gemm_body(const GemmArgs& g, int w, float* smem, const AdamEpi* ae = nu
 #pragma unroll
     for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, BRC>(rB, ldb, p, j0, 0);
 #pragma unroll
-    for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, ARC>(As0, p, ra[p]);
+    for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, ARC, RP>(As0, p, ra[p]);
 #pragma unroll
-    for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC>(Bs0, p, rb[p]);
+    for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC, RP>(Bs0, p, rb[p]);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const float* Ac = (kt & 1) ? As1 : As0;
@@ -527,15 +544,33 @@ DEV void gemm_body(const GemmArgs& g, int w, float* smem, const AdamEpi* ae = nu
         __builtin_amdgcn_sched_barrier(0);
         // all fragments of the slice first, then the MFMA chain
         float av[BK / 2][TM], bv[BK / 2][TN];
+        if constexpr (KB) {
+            // k-blocked: MFMA kk of lane half lh takes k = 8 lh + kk (BK = 16)
 #pragma unroll
-        for (int kk = 0; kk < BK / 2; ++kk) {
-            const int rr = 2 * kk + lh;
+            for (int a = 0; a < TM; ++a) {
+                const float* r = Ac + (wi + a * 32 + l32) * RP + 8 * lh;
+                const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
+                av[0][a] = x0.x; av[1][a] = x0.y; av[2][a] = x0.z; av[3][a] = x0.w;
+                av[4][a] = x1.x; av[5][a] = x1.y; av[6][a] = x1.z; av[7][a] = x1.w;
+            }
 #pragma unroll
-            for (int a = 0; a < TM; ++a)
-                av[kk][a] = ARC ? Ac[(wi + a * 32 + l32) * (BK + 1) + rr] : Ac[rr * BM + wi + a * 32 + l32];
+            for (int b = 0; b < TN; ++b) {
+                const float* r = Bc + (wj + b * 32 + l32) * RP + 8 * lh;
+                const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
+                bv[0][b] = x0.x; bv[1][b] = x0.y; bv[2][b] = x0.z; bv[3][b] = x0.w;
+                bv[4][b] = x1.x; bv[5][b] = x1.y; bv[6][b] = x1.z; bv[7][b] = x1.w;
+            }
+        } else {
 #pragma unroll
-            for (int b = 0; b < TN; ++b)
-                bv[kk][b] = BRC ? Bc[(wj + b * 32 + l32) * (BK + 1) + rr] : Bc[rr * BN + wj + b * 32 + l32];
+            for (int kk = 0; kk < BK / 2; ++kk) {
+                const int rr = 2 * kk + lh;
+#pragma unroll
+                for (int a = 0; a < TM; ++a)
+                    av[kk][a] = ARC ? Ac[(wi + a * 32 + l32) * RP + rr] : Ac[rr * BM + wi + a * 32 + l32];
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    bv[kk][b] = BRC ? Bc[(wj + b * 32 + l32) * RP + rr] : Bc[rr * BN + wj + b * 32 + l32];
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -552,9 +587,9 @@ DEV void gemm_body(const GemmArgs& g, int w, float* smem, const AdamEpi* ae = nu
         float* An = (kt & 1) ? As0 : As1;
         float* Bn = (kt & 1) ? Bs0 : Bs1;
 #pragma unroll
-        for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, ARC>(An, p, ra[p]);
+        for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, ARC, RP>(An, p, ra[p]);
 #pragma unroll
-        for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC>(Bn, p, rb[p]);
+        for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC, RP>(Bn, p, rb[p]);
         __syncthreads();
     }
 
@@ -619,9 +654,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs g) {
 // gradient tile (BM rows of BN + 1) when that is larger (BK = 16 slices)
 template <int BM, int BN, int BK, bool ARC, bool BRC, int EPI>
 constexpr int group_smem_floats() {
-    return (EPI == EPI_ADAM && BM * (BN + 1) > gemm_smem_floats<BM, BN, BK, ARC, BRC>())
-               ? BM * (BN + 1)
-               : gemm_smem_floats<BM, BN, BK, ARC, BRC>();
+    constexpr int G = gemm_smem_floats<BM, BN, BK, ARC, BRC, gemm_kb<BM, BN, BK, ARC, BRC, EPI>()>();
+    return (EPI == EPI_ADAM && BM * (BN + 1) > G) ? BM * (BN + 1) : G;
 }
 
 template <int BM, int BN, bool ARC, bool BRC, int EPI, int BK>
