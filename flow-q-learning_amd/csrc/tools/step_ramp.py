@@ -1,6 +1,9 @@
 """Step rate right after setup, in chunks (developer tool, on the GPU box):
 
-  python flow-q-learning_amd/csrc/tools/step_ramp.py [chunk] [n_chunks] [idle_s] [preheat_ms]
+  python flow-q-learning_amd/csrc/tools/step_ramp.py [chunk] [n_chunks] [idle_s] [preheat_ms] [mem]
+
+(mem = 1: the preheat also streams HBM: device-to-device copies of a 1 GB buffer on a side
+stream while the dominant kernel replays)
 
 Builds the bench population (cube, 16 members, 1M rows), runs 5 warmup steps, then
 times n_chunks back-to-back chunks of `chunk` steps (host-synchronised each), then
@@ -26,6 +29,7 @@ def main():
     n_chunks = int(sys.argv[2]) if len(sys.argv) > 2 else 12
     idle = float(sys.argv[3]) if len(sys.argv) > 3 else 1.0
     preheat_ms = float(sys.argv[4]) if len(sys.argv) > 4 else 0.0
+    mem = len(sys.argv) > 5 and sys.argv[5] == "1"
     torch.cuda.set_device(0)
     wl = bench.WORKLOADS["cube"]
     data = bench.synthetic_dataset(1_000_000, wl["obs_dim"], wl["action_dim"])
@@ -35,7 +39,15 @@ def main():
     pop.set_dataset(data)
     if preheat_ms > 0:  # as bench.py --preheat-ms
         us, _ = pop.time_dominant_kernel(1)
+        if mem:
+            src = torch.empty(256 << 20, dtype=torch.float32, device="cuda")
+            dst = torch.empty_like(src)
+            side = torch.cuda.Stream()
+            with torch.cuda.stream(side):
+                for _ in range(int(preheat_ms / 0.35)):  # ~2 GB moved per copy, ~0.35 ms at ~6 TB/s
+                    dst.copy_(src)
         pop.time_dominant_kernel(max(1, int(preheat_ms * 1e3 / us)))
+        torch.cuda.synchronize()
     pop.step(5)
     pop.sync()
 
