@@ -1076,7 +1076,12 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
             float4 bias4[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) bias4[r] = bload4(rW, (int)g.b_off[l] + 64 * w + 16 * lk + 4 * r);
-            ef_kloop(acc, ring, rW, xs, NS, (int)g.w_off[l], (int)g.w_off[nl], lo, lk, li);
+            // both layer offsets waited for here, with the bias loads' scalar loads: an SMEM
+            // load left in flight into the k-loop made its first LDS wait lgkmcnt(0) (SMEM
+            // returns out of order), exposing a B-fragment read every 8 k-steps
+            const int wcur = (int)g.w_off[l], wnext = (int)g.w_off[nl];
+            asm volatile("" ::"s"(wcur), "s"(wnext));
+            ef_kloop(acc, ring, rW, xs, NS, wcur, wnext, lo, lk, li);
             // tile c, reg r, lane (lk, li): feature 64w + 4(4lk + r) + c, column li
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
