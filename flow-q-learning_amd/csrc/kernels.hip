@@ -1375,7 +1375,9 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
         const float pb = P[g.b_off[l] + tid];
         const float pg = LN ? P[g.g_off[l] + tid] : 0.f;
         const float pe = LN ? P[g.be_off[l] + tid] : 0.f;
-        ef_kloop(acc, ring, rW, xs, NS, (int)g.w_off[l], (int)g.w_off[nl], lo, lk, li);
+        const int wcur = (int)g.w_off[l], wnext = (int)g.w_off[nl];
+        asm volatile("" ::"s"(wcur), "s"(wnext));  // no SMEM load in flight into the k-loop (see euler_flow_kernel)
+        ef_kloop(acc, ring, rW, xs, NS, wcur, wnext, lo, lk, li);
         lnp[0][tid] = pb;
         if constexpr (LN) {
             lnp[1][tid] = pg;
