@@ -1756,7 +1756,21 @@ DEV float row16_sum(float v) {
     v += dpp_mov<0x140>(v);
     return v;
 }
-// Sum over lk (lanes li, li+16, li+32, li+48).
+// Reduce-scatter over the 16 lanes of a DPP row: lane li of the row returns the sum of
+// v[li] over the row's lanes (butterfly on li's bits 3..0: row_ror:8, row_half_mirror,
+// quad_perm [2,3,0,1], quad_perm [1,0,3,2]; each level keeps the half named by the bit
+// and adds the partner's other half). 45 VALU, no LDS.
+DEV float row16_reduce_scatter(const float (&v)[16], int li) {
+    const bool b3 = li & 8, b2 = li & 4, b1 = li & 2, b0 = li & 1;
+    float a[8], b[4], c[2];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = (b3 ? v[j + 8] : v[j]) + dpp_mov<0x128>(b3 ? v[j] : v[j + 8]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = (b2 ? a[j + 4] : a[j]) + dpp_mov<0x141>(b2 ? a[j] : a[j + 4]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) c[j] = (b1 ? b[j + 2] : b[j]) + dpp_mov<0x4E>(b1 ? b[j] : b[j + 2]);
+    return (b0 ? c[1] : c[0]) + dpp_mov<0xB1>(b0 ? c[0] : c[1]);
+}
 
 bool stream_bwd_supported(int H, int L, int nout, int M, int Mg) {
     return H == EF_H && L >= 1 && L <= EF_MAX_LAYERS && nout >= 1 && nout <= 8 && M % EF_NC == 0 &&
@@ -1770,7 +1784,6 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
     __shared__ __attribute__((aligned(16))) float scr[H * NC];         // head kernel W_L [H][nout]; then LN-grad products
     __shared__ float colred[2][EF_NW][NC];                            // LN column-stat partials per wave
     __shared__ float dos[8][NC];                                      // dout of the block's columns
-    __shared__ __attribute__((aligned(16))) float gams[H];            // LN scale of the current layer
 
     const int tiles = g.M / NC;
     const int total = tiles * g.ny * g.nz;
@@ -1848,7 +1861,7 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
 
     // epilogue inputs of layer l (u, LN stats, LN scale), loaded one layer ahead
     // so that their latency hides under the previous dX product
-    float u[4][4], gth = 0.f, mu = 0.f, rs = 0.f;  // gth: LN scale of feature tid (staged through LDS)
+    float u[4][4], mu = 0.f, rs = 0.f;
     // (lane indices as arguments: inside the layer loop they come from an opaque copy of
     // tid, so that per-lane addresses are recomputed where they are used instead of
     // being hoisted out of the loop and spilled: every spill reload was a vmcnt(0) that
@@ -1863,7 +1876,6 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         if constexpr (LN) {
             mu = bload1(make_rsrc(g.MU[l] + sto, NC), li_ * 4, 0);
             rs = bload1(make_rsrc(g.RS[l] + sto, NC), li_ * 4, 0);
-            gth = bload1(rPe, tid_ * 4, (int)g.g_off[l] * 4);
         }
     };
     load_epi(L - 1, tid, li, lk);
@@ -1902,30 +1914,29 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         float* const scr_l = scr + (64 * w + 16 * lk_l) * NC + li_l;
         // ---- du_l from dh = dL/dG_l (GELU', LayerNorm backward), in place in dh ----
         if constexpr (LN) {
-            gams[tid_l] = gth;
-            // pass 1: xhat, GELU' (kept in u); dh and dh * xhat to LDS (LN bias / scale grads;
-            // the slab is free: the previous product is done with it)
-            float xh[4][4];
+            // this lane's 16 LN scales (features 64w + 16lk + 4r + c), in flight during the
+            // DPP reduction and the GELU math below
+            float4 gq[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < 4; ++r) gq[r] = bload4(rPe, (int)g.g_off[l] + 64 * w + 16 * lk_l + 4 * r);
+            // LN bias grads: feature 64w + 16lk + li = tid_l, sum over the block's columns of
+            // dh (DPP reduce-scatter over the column lanes; done before xhat is live)
+            if (gp) bstore1(rPart, row16_reduce_scatter(reinterpret_cast<const float(&)[16]>(dh), li_l), tid_l * 4,
+                            (2 * L + l) * H * 4);
+            // pass 1: xhat, GELU' (kept in u); dh * xhat to LDS (LN scale grads, thread =
+            // feature); the column partials of dh*gamma and dh*gamma*xhat. No slab write and
+            // no barrier before the column stats: the previous product needs no barrier after it
+            float xh[4][4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float gr[4] = {gq[r].x, gq[r].y, gq[r].z, gq[r].w};
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     float gv, gpr;
                     gelu_and_grad_fast(u[r][c], gv, gpr);
                     u[r][c] = gpr;
                     xh[r][c] = (gv - mu) * rs;
-                    scr_l[(4 * r + c) * NC] = dh[r][c];
-                    slab_l[(4 * r + c) * NC] = dh[r][c] * xh[r][c];
-                }
-            __syncthreads();  // gams, scr, slab visible
-            // column partials of dh*gamma and dh*gamma*xhat
-            float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float4 g4 = *reinterpret_cast<const float4*>(&gams[64 * w + 16 * lk_l + 4 * r]);
-                const float gr[4] = {g4.x, g4.y, g4.z, g4.w};
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
+                    scr_l[(4 * r + c) * NC] = dh[r][c] * xh[r][c];
                     dh[r][c] *= gr[c];  // dh * gamma from here on
                     s1 += dh[r][c];
                     s2 += dh[r][c] * xh[r][c];
@@ -1937,11 +1948,8 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
                 colred[0][w][li_l] = s1;
                 colred[1][w][li_l] = s2;
             }
-            if (gp) {
-                bstore1(rPart, row_sum(scr, tid_l), tid_l * 4, (2 * L + l) * H * 4);   // LN bias: sum dh
-                bstore1(rPart, row_sum(slab, tid_l), tid_l * 4, (L + l) * H * 4);      // LN scale: sum dh * xhat
-            }
-            __syncthreads();  // colred visible; scr, slab free
+            __syncthreads();  // colred, scr visible
+            if (gp) bstore1(rPart, row_sum(scr, tid_l), tid_l * 4, (L + l) * H * 4);  // LN scale: sum dh * xhat
             float c1 = 0.f, c2 = 0.f;
 #pragma unroll
             for (int q8 = 0; q8 < EF_NW; ++q8) {
@@ -2010,7 +2018,10 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int c = 0; c < 4; ++c) dh[r][c] = acc[c][r];
-        __syncthreads();  // every wave done with slab / colred
+        // the actor variant writes the slab right away (du of the next layer): wait for every
+        // wave's product; the LN variant's next LDS writes (scr, colred) are not read by the
+        // product, and its slab write follows the next barrier
+        if constexpr (!LN) __syncthreads();
     }
 }
 
