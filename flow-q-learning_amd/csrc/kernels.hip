@@ -1361,6 +1361,12 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
     for (int p = 0; p < PF; ++p) ring[p] = bload4(rW, (int)g.w_off[0] + 4 * p * H + lo);
     const bool st = c0 >= g.st_lo && c0 + NC <= g.st_hi;  // block stores activations
     const int m = c0 + li;
+    if constexpr (LN) {
+        // LN variant: layer l's bias / LN scale / LN bias are staged one layer ahead (see below)
+        lnp[0][tid] = P[g.b_off[0] + tid];
+        lnp[1][tid] = P[g.g_off[0] + tid];
+        lnp[2][tid] = P[g.be_off[0] + tid];
+    }
     __syncthreads();
 
     for (int l = 0; l < L; ++l) {
@@ -1370,20 +1376,22 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
         f32x4 acc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // this lane's 16 features 64w + 16lk + 4r + c: bias (and LN scale / bias) in flight during the k-loop
-        // feature tid's bias / LN scale / LN bias, in flight during the k-loop, then to LDS
-        const float pb = P[g.b_off[l] + tid];
-        const float pg = LN ? P[g.g_off[l] + tid] : 0.f;
-        const float pe = LN ? P[g.be_off[l] + tid] : 0.f;
+        // feature tid's bias (LN: and LN scale / bias) in flight during the k-loop, then to LDS.
+        // LN: those of the NEXT layer, written after this layer's barriers that retire the
+        // current ones (bias after the stats barrier, scale / bias after the slab barrier), so
+        // that no barrier is needed between the k-loop and the epilogue: the stats barrier
+        // already orders every wave's slab reads before the slab writes
+        const int lp = LN ? nl : l;
+        const float pb = P[g.b_off[lp] + tid];
+        const float pg = LN ? P[g.g_off[lp] + tid] : 0.f;
+        const float pe = LN ? P[g.be_off[lp] + tid] : 0.f;
         const int wcur = (int)g.w_off[l], wnext = (int)g.w_off[nl];
         asm volatile("" ::"s"(wcur), "s"(wnext));  // no SMEM load in flight into the k-loop (see euler_flow_kernel)
         ef_kloop(acc, ring, rW, xs, NS, wcur, wnext, lo, lk, li);
-        lnp[0][tid] = pb;
-        if constexpr (LN) {
-            lnp[1][tid] = pg;
-            lnp[2][tid] = pe;
+        if constexpr (!LN) {
+            lnp[0][tid] = pb;
+            __syncthreads();  // every wave is done reading the slab; lnp visible
         }
-        __syncthreads();  // every wave is done reading the slab; lnp visible
 
         // activation stores: buffer ops, per-lane offset + wave-uniform row offset (no 64-bit address VGPRs)
         const bool stU = st && g.U[l], stG = st && g.G[l] && c0 + NC <= g.g_hi;
@@ -1418,7 +1426,8 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
                 lnred[0][w][li] = s1;
                 lnred[1][w][li] = s2;
             }
-            __syncthreads();
+            __syncthreads();  // lnred visible; every wave is done reading the slab and lnp[0]
+            lnp[0][tid] = pb;  // next layer's bias (visible after the slab barrier)
             float S1 = 0.f, S2 = 0.f;
 #pragma unroll
             for (int q = 0; q < EF_NW; ++q) {
@@ -1452,6 +1461,10 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
                 slab[f * NC + li] = v[r][c];
             }
         __syncthreads();
+        if constexpr (LN) {
+            lnp[1][tid] = pg;  // next layer's LN scale / bias (visible after its stats barrier)
+            lnp[2][tid] = pe;
+        }
     }
     // head: out[j][col] = sum_k W_L[k][j] h[k][col] + b_L[j]
     {
