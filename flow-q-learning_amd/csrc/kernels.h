@@ -221,7 +221,12 @@ struct StreamBwdArgs {
     int ld_da, D0, na;
     int ny, nz;
     const int* slots;
+    // optional diagnostics (FQLPOP_PHASE_PROBE): per block [SB_PHASE_STRIDE] s_memrealtime stamps:
+    // [0] start, [1] end, then per layer pass (L-1-l): top, stats barrier in/out, slab barrier out,
+    // product done
+    unsigned long long* phase;
 };
+constexpr int SB_PHASE_STRIDE = 48;
 bool stream_bwd_supported(int H, int L, int nout, int M, int Mg);
 void launch_stream_bwd(bool ln, const StreamBwdArgs& a, hipStream_t s);
 // Partial index layout of StreamBwdArgs::part (per tile):

@@ -1822,55 +1822,13 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
     // 64-bit per-lane addresses to keep live across the layer loop)
     const rsrc_t rPart = make_rsrc(gp ? part : g.params, gp ? g.NP : 0);
     const rsrc_t rPe = make_rsrc(P, g.ens);
+    // diagnostics only (null unless FQLPOP_PHASE_PROBE): wave 0's view of the phases
+    unsigned long long* const ph = g.phase != nullptr ? g.phase + (long long)blockIdx.x * SB_PHASE_STRIDE : nullptr;
+    auto stamp = [&](int i) {
+        if (ph != nullptr && tid == 0) ph[i] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
 
-    if (tid < nout * NC) {
-        const int j = tid / NC, col = tid % NC;
-        dos[j][col] = g.dout[(long long)slot * g.dout_ss + (long long)y * g.dout_sy + (long long)j * g.ld_o + c0 + col];
-    }
-    {
-        // head kernel W_L [H][nout] (nout <= 8): unguarded loads (past H*nout: 0), then stores
-        const rsrc_t rH = make_rsrc(P + g.w_off[L], (long long)H * nout);
-        float hv[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) hv[q] = bload1(rH, (tid + q * NT) * 4, 0);
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (tid + q * NT < H * nout) scr[tid + q * NT] = hv[q];
-    }
-    __syncthreads();
-
-    // head kernel grad partials (thread = feature): sum_col G_{L-1}[k][col] dout[j][col]
-    if (gp) {
-        const float* __restrict__ gr = g.Ghead + so + (long long)tid * g.ld_s;
-        float gv[NC];
-#pragma unroll
-        for (int q = 0; q < NC / 4; ++q) {
-            const float4 t4 = *reinterpret_cast<const float4*>(gr + 4 * q);
-            gv[4 * q] = t4.x; gv[4 * q + 1] = t4.y; gv[4 * q + 2] = t4.z; gv[4 * q + 3] = t4.w;
-        }
-        const int w5 = (LN ? 3 : 1) * L * H;
-        for (int j = 0; j < nout; ++j) {
-            float v = 0.f;
-#pragma unroll
-            for (int col = 0; col < NC; ++col) v += gv[col] * dos[j][col];
-            part[w5 + tid * nout + j] = v;
-        }
-    }
-    // lane layout (as ef_kloop's accumulators): column li, features f = 64w + 16lk + 4r + c
-    // last hidden layer: dh = W_L dout (nout <= 8, VALU)
-    float dh[4][4];  // [r][c]
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int f = 64 * w + 16 * lk + 4 * r + c;
-            float s = 0.f;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j < nout) s += scr[f * nout + j] * dos[j][li];
-            dh[r][c] = s;
-        }
-    __syncthreads();  // scr (head kernel image) is reused by the first epilogue
 
     // epilogue inputs of layer l (u, LN stats, LN scale), loaded one layer ahead
     // so that their latency hides under the previous dX product
@@ -1891,17 +1849,97 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
             rs = bload1(make_rsrc(g.RS[l] + sto, NC), li_ * 4, 0);
         }
     };
-    load_epi(L - 1, tid, li, lk);
     // W^T ring: the first PF k-steps of the first dX product (W_{L-1}^T), issued after the
     // epilogue loads as in the layer loop, so that the loop head waits for the epilogue
     // loads only (vmcnt(PF)) instead of for everything in flight (a vmcnt(0) that also
     // waited for the ring refills of the next product, every layer)
     const int lo = lk * H + 64 * w + 4 * li;
     float4 ring[PF];
-    {
+    auto load_first = [&]() {
+        load_epi(L - 1, tid, li, lk);
         const int wf = L > 1 ? (int)g.wt_off[L - 1] : 0;
 #pragma unroll
         for (int p = 0; p < PF; ++p) ring[p] = bload4(rT, wf + 4 * p * H + lo);
+    };
+    // lane layout (as ef_kloop's accumulators): column li, features f = 64w + 16lk + 4r + c
+    // last hidden layer: dh = W_L dout (nout <= 8, VALU)
+    float dh[4][4];  // [r][c]
+    const int w5 = (LN ? 3 : 1) * L * H;  // head kernel grads in the partials
+    load_first();
+    if (nout == 1) {
+        // (the critic: a scalar head) no LDS staging: W_L[f] as float4 runs, this lane's dout,
+        // and G_{L-1} in the accumulator layout, all issued right after the first layer's
+        // epilogue inputs and ring (one memory round trip, no barrier); the head
+        // kernel grads sum_col G_{L-1}[f][col] dout[col] by the DPP reduce-scatter over the
+        // column lanes (lane li ends with feature 64w + 16lk + li = tid)
+        const rsrc_t rH = make_rsrc(P + g.w_off[L], (long long)H);
+        float4 wl[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wl[r] = bload4(rH, 64 * w + 16 * lk + 4 * r);
+        const float dv = g.dout[(long long)slot * g.dout_ss + (long long)y * g.dout_sy + c0 + li];
+        float gh[16];
+        if (gp) {
+            const rsrc_t rG = make_rsrc(g.Ghead + so, (long long)H * g.ld_s);
+            const int vo = ((64 * w + 16 * lk) * g.ld_s + li) * 4;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) gh[e] = bload1(rG, vo, e * g.ld_s * 4);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float wv[4] = {wl[r].x, wl[r].y, wl[r].z, wl[r].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) dh[r][c] = 0.f + wv[c] * dv;  // as the general path's sum
+        }
+        if (gp) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) gh[e] *= dv;
+            bstore1(rPart, row16_reduce_scatter(gh, li), tid * 4, w5 * 4);
+        }
+    } else {
+        if (tid < nout * NC) {
+            const int j = tid / NC, col = tid % NC;
+            dos[j][col] = g.dout[(long long)slot * g.dout_ss + (long long)y * g.dout_sy + (long long)j * g.ld_o + c0 + col];
+        }
+        {
+            // head kernel W_L [H][nout] (nout <= 8): unguarded loads (past H*nout: 0), then stores
+            const rsrc_t rH = make_rsrc(P + g.w_off[L], (long long)H * nout);
+            float hv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) hv[q] = bload1(rH, (tid + q * NT) * 4, 0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (tid + q * NT < H * nout) scr[tid + q * NT] = hv[q];
+        }
+        __syncthreads();
+
+        // head kernel grad partials (thread = feature): sum_col G_{L-1}[k][col] dout[j][col]
+        if (gp) {
+            const float* __restrict__ gr = g.Ghead + so + (long long)tid * g.ld_s;
+            float gv[NC];
+#pragma unroll
+            for (int q = 0; q < NC / 4; ++q) {
+                const float4 t4 = *reinterpret_cast<const float4*>(gr + 4 * q);
+                gv[4 * q] = t4.x; gv[4 * q + 1] = t4.y; gv[4 * q + 2] = t4.z; gv[4 * q + 3] = t4.w;
+            }
+            for (int j = 0; j < nout; ++j) {
+                float v = 0.f;
+#pragma unroll
+                for (int col = 0; col < NC; ++col) v += gv[col] * dos[j][col];
+                part[w5 + tid * nout + j] = v;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int f = 64 * w + 16 * lk + 4 * r + c;
+                float s = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j < nout) s += scr[f * nout + j] * dos[j][li];
+                dh[r][c] = s;
+            }
+        __syncthreads();  // scr (head kernel image) is reused by the first epilogue
     }
     // parameter-grad partials, thread = feature: sums over the block's 16 columns of an LDS image
     auto row_sum = [&](const float* a, int tid_) {
@@ -1925,6 +1963,8 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         // (r, c) is at + (4r + c) * NC (ds_write immediate offsets, one address VGPR)
         float* const slab_l = slab + (64 * w + 16 * lk_l) * NC + li_l;
         float* const scr_l = scr + (64 * w + 16 * lk_l) * NC + li_l;
+        const int pi = 2 + 5 * (L - 1 - l);
+        stamp(pi);
         // ---- du_l from dh = dL/dG_l (GELU', LayerNorm backward), in place in dh ----
         if constexpr (LN) {
             // this lane's 16 LN scales (features 64w + 16lk + 4r + c), in flight during the
@@ -1961,7 +2001,9 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
                 colred[0][w][li_l] = s1;
                 colred[1][w][li_l] = s2;
             }
+            stamp(pi + 1);
             __syncthreads();  // colred, scr visible
+            stamp(pi + 2);
             if (gp) bstore1(rPart, row_sum(scr, tid_l), tid_l * 4, (L + l) * H * 4);  // LN scale: sum dh * xhat
             float c1 = 0.f, c2 = 0.f;
 #pragma unroll
@@ -2001,14 +2043,29 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
                 for (int c = 0; c < 4; ++c) slab_l[(4 * r + c) * NC] = dh[r][c];
         }
         __syncthreads();
+        stamp(pi + 3);
         if (gp) bstore1(rPart, row_sum(slab, tid_l), tid_l * 4, l * H * 4);  // bias: sum du
         if (l == 0 && g.da != nullptr && !gp) {
             // dQ/da for the actor's Q-loss columns (replaces input_grad_kernel): output (j, col)
             // = thread & 127, feature quarter = thread >> 7, then a fixed-order fold in scr
+            // W_0's action rows D0 .. D0 + na - 1 (na H <= 8 NT floats) staged into scr (free
+            // after the slab barrier) with one batch of loads, instead of one dependent L2
+            // round trip per 8 features in the loop below
             const int o = tid_l & 127, q = tid_l >> 7, j = o >> 4, col = o & 15;
+            float* const wa = scr + 512;
+            {
+                const rsrc_t rA = make_rsrc(P + g.w_off[0] + (long long)g.D0 * H, (long long)g.na * H);
+                float t[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) t[i] = bload1(rA, (tid_l + i * NT) * 4, 0);  // past na H: 0
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (tid_l + i * NT < g.na * H) wa[tid_l + i * NT] = t[i];
+            }
+            __syncthreads();
             float s = 0.f;
             if (j < g.na) {
-                const float* __restrict__ wr = P + g.w_off[0] + (long long)(g.D0 + j) * H;
+                const float* const wr = wa + j * H;
 #pragma unroll 8
                 for (int f = q * (H / 4); f < (q + 1) * (H / 4); ++f) s = fmaf(wr[f], slab[f * NC + col], s);
             }
@@ -2031,11 +2088,13 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int c = 0; c < 4; ++c) dh[r][c] = acc[c][r];
+        stamp(pi + 4);
         // the actor variant writes the slab right away (du of the next layer): wait for every
         // wave's product; the LN variant's next LDS writes (scr, colred) are not read by the
         // product, and its slab write follows the next barrier
         if constexpr (!LN) __syncthreads();
     }
+    stamp(1);
 }
 
 void launch_stream_bwd(bool ln, const StreamBwdArgs& a, hipStream_t s) {

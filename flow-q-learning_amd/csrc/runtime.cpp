@@ -221,6 +221,11 @@ struct fqlpop {
     long long probe_step = 0;
     unsigned long long* probe_slots = nullptr;   // [2 sets][pairs][probe_blocks][2] (device view)
     unsigned long long* probe_host = nullptr;    // the same slots: mapped coherent host memory
+    // FQLPOP_PHASE_PROBE=1 (diagnostics): the critic backward's per-block phase stamps (mapped
+    // host memory, overwritten by every launch; summarised on stderr at destroy)
+    unsigned long long* phase_host = nullptr;
+    unsigned long long* phase_dev = nullptr;
+    long long phase_blocks = 0;
     int probe_pairs = 0;
     long long probe_blocks = 0;                  // max blocks of one dominant-kernel launch
     int probe_nz[2] = {0, 0};                    // active members of the step that used each set
@@ -645,8 +650,13 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
     if (ig) {
         // the critic's dQ/da, computed by the backward's layer-0 epilogue (per-ensemble partials)
         ARGCHK(ig->off == Mg && ig->M == M - Mg, "input-grad columns must follow the grad columns");
+        ARGCHK(ig->A >= 1 && ig->A <= 8, "fused dQ/da: at most 8 action inputs");
         a.da = ig->da.p; a.da_ss = ig->da.ss; a.da_sy = (long long)ig->A * ig->M;
         a.ld_da = ig->M; a.D0 = ig->D; a.na = ig->A;
+    }
+    if (&N == &h->critic && h->phase_dev != nullptr) {
+        ARGCHK((long long)(M / 16) * N.E * c.nz <= h->phase_blocks, "phase probe: too many blocks");
+        a.phase = h->phase_dev;
     }
     if (!(skip_mask() & (&N == &h->critic ? 32 : &N == &h->bc ? 64 : 128))) launch_stream_bwd(N.ln, a, s);
     hipEvent_t ev = nullptr;
@@ -860,6 +870,39 @@ double dominant_flops(const fqlpop* h) {
     if (h->euler_fused)
         return (h->S - 1) * 2.0 * B * (K0 * H + (h->L - 1) * H * H + H * A) * h->nz;
     return 2.0 * H * B * H * h->nz;
+}
+
+// FQLPOP_PHASE_PROBE: mean phase durations (us) of the critic backward's last launch, from
+// wave 0's stamps of every block (s_memrealtime, 100 MHz)
+void phase_report(const unsigned long long* ph, long long nb, int L) {
+    long long t0 = -1, t1 = 0, n = 0;
+    double blk = 0, pro = 0, tail = 0, pass1[8] = {}, wait2[8] = {}, p2[8] = {}, prod[8] = {};
+    for (long long b = 0; b < nb; ++b) {
+        const unsigned long long* p = ph + b * SB_PHASE_STRIDE;
+        if (p[0] == 0 || p[1] < p[0]) continue;
+        ++n;
+        t0 = t0 < 0 ? (long long)p[0] : std::min(t0, (long long)p[0]);
+        t1 = std::max(t1, (long long)p[1]);
+        blk += (double)(p[1] - p[0]);
+        pro += (double)(p[2] - p[0]);
+        tail += (double)(p[1] - p[2 + 5 * (L - 1) + 3]);
+        for (int i = 0; i < L && i < 8; ++i) {
+            const unsigned long long* q = p + 2 + 5 * i;
+            pass1[i] += (double)(q[1] - q[0]);
+            wait2[i] += (double)(q[2] - q[1]);
+            p2[i] += (double)(q[3] - q[2]);
+            if (i + 1 < L) prod[i] += (double)(q[4] - q[3]);
+        }
+    }
+    if (n == 0) return;
+    const double us = 0.01 / (double)n;  // 100 MHz ticks -> us, averaged over blocks
+    std::fprintf(stderr,
+                 "phase probe (critic backward, last launch): %lld blocks, span %.1f us, block %.2f us "
+                 "(prologue %.2f, after the last slab barrier %.2f)\n",
+                 n, (double)(t1 - t0) * 0.01, blk * us, pro * us, tail * us);
+    for (int i = 0; i < L && i < 8; ++i)
+        std::fprintf(stderr, "  pass %d: LN pass 1 %.2f | stats barrier %.2f | pass 2 + du + slab barrier %.2f | dX product %.2f\n",
+                     i, pass1[i] * us, wait2[i] * us, p2[i] * us, prod[i] * us);
 }
 
 // Enqueue one population update (train) or one total_loss pass (!train).
@@ -1393,6 +1436,13 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         // event, with no device-to-host copy (a copy kernel) interleaved with the steps
         const size_t pb = sizeof(unsigned long long) * 4 * h->probe_blocks * h->probe_pairs;
         HIPCHK(hipHostMalloc((void**)&h->probe_host, pb, hipHostMallocMapped | hipHostMallocCoherent));
+        if (const char* e = std::getenv("FQLPOP_PHASE_PROBE"); e != nullptr && e[0] == '1') {
+            h->phase_blocks = (long long)(2 * cfg->batch_size / 16) * 2 * n_members;  // critic: 2B columns, 2 members
+            const size_t phb = sizeof(unsigned long long) * SB_PHASE_STRIDE * h->phase_blocks;
+            HIPCHK(hipHostMalloc((void**)&h->phase_host, phb, hipHostMallocMapped | hipHostMallocCoherent));
+            std::memset(h->phase_host, 0, phb);
+            HIPCHK(hipHostGetDevicePointer((void**)&h->phase_dev, h->phase_host, 0));
+        }
         std::memset(h->probe_host, 0, pb);
         HIPCHK(hipHostGetDevicePointer((void**)&h->probe_slots, h->probe_host, 0));
         for (auto& e : h->probe_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1515,6 +1565,11 @@ int fqlpop_destroy(fqlpop_t* h) {
             if (e) (void)hipEventDestroy(e);
         if (h->probe_stream) (void)hipStreamDestroy(h->probe_stream);
         if (h->probe_host) (void)hipHostFree(h->probe_host);
+        if (h->phase_host) {
+            (void)hipDeviceSynchronize();
+            phase_report(h->phase_host, h->phase_blocks, h->L);
+            (void)hipHostFree(h->phase_host);
+        }
         if (h->sX && h->sX != h->sM) (void)hipStreamDestroy(h->sX);
         if (h->sF && h->sF != h->sM) (void)hipStreamDestroy(h->sF);
         if (h->sB && h->sB != h->sM) (void)hipStreamDestroy(h->sB);
