@@ -87,7 +87,8 @@ struct AdamEpi {
     int n_total_chunks;
     const int* count;
     float lr, tau;
-    int mode;                         // 0; timing probes (FQLPOP_DW_MODE): 1 = no optimiser pass, 2 = one k-slice
+    int mode;                         // 0; timing probes (FQLPOP_DW_MODE): 1 = no optimiser pass, 2 = one k-slice,
+                                      // 3 = no W^T pass
     int nt;                           // non-temporal optimiser streams: 1 m/v, 2 target, 4 p_in, 8 p_out/W^T
     // the net's small leaves (biases, LN, head) ride in the same launch: blocks past the
     // GEMM tiles run the adam_kernel body on small.ids chunks (small_blocks = chunks x nz)

@@ -449,7 +449,7 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
     }
     // pass 2 (hidden layers: M = H, full tiles): W^T[j][i0 .. i0+BM) as float4 runs along i
     const int nt = e.nt;
-    if (e.wt_off[gi] >= 0 && e.mode != 1) {
+    if (e.wt_off[gi] >= 0 && e.mode != 1 && e.mode != 3) {  // mode 3: timing probe without the W^T pass
         float* __restrict__ WT = e.wt_out + (long long)slot * e.PTT + e.wt_off[gi] + (long long)y * e.wt_sy;
         constexpr int TPC = BM / 4;  // threads per W^T row segment
 #pragma unroll 4

@@ -715,6 +715,7 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         {
             const char* dm = std::getenv("FQLPOP_DW_MODE");
             ae.mode = dm ? std::atoi(dm) : 0;
+            if (ae.mode == 4) ae.mode = ni == 0 ? 0 : 3;  // timing probe: no W^T pass for the actor nets
             // m, v and the target stream non-temporally: read and written once per step, they
             // need not displace the weights the streamed kernels re-read from L2 / MALL
             // (+1.0 % same-box; FQLPOP_ADAM_NT: bit mask, see AdamEpi::nt)
