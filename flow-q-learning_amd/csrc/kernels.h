@@ -126,7 +126,10 @@ struct EulerArgs {
     int nz;
     const int* slots;
     unsigned long long* probe;            // optional per-block {start, end} stamps
+    unsigned long long* phase;            // diagnostics (FQLPOP_PHASE_PROBE): [EF_PHASE_STRIDE] per block
 };
+// per block: [0] start, then per (step, layer) k-loop start / k-loop end / epilogue end / barrier out
+constexpr int EF_PHASE_STRIDE = 4 * 10 * (EF_MAX_LAYERS + 1) + 8;
 bool euler_flow_supported(int H, int L, int D, int A, int B);
 void launch_euler_flow(const EulerArgs& a, hipStream_t s);
 

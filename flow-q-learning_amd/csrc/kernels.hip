@@ -1039,6 +1039,15 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
     if (g.probe != nullptr && tid == 0) g.probe[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#ifdef FQ_PHASE_PROBE  // diagnostic build only (make PHASE=1): the disabled branch cost 0.3 % in the step
+    unsigned long long* const ph = g.phase != nullptr ? g.phase + (long long)blockIdx.x * EF_PHASE_STRIDE : nullptr;
+    auto stamp = [&](int i) {
+        if (ph != nullptr && tid == 0) ph[i] = __builtin_amdgcn_s_memrealtime();
+    };
+#else
+    auto stamp = [](int) {};
+#endif
+    stamp(0);
 
     const int D = g.D, A = g.A, L = g.L, B = g.B, S = g.S;
     const int K0 = D + A + 1, NS0 = (K0 + 4 * PF - 1) / (4 * PF) * PF;  // padded k-steps of layer 0
@@ -1081,7 +1090,10 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
             // returns out of order), exposing a B-fragment read every 8 k-steps
             const int wcur = (int)g.w_off[l], wnext = (int)g.w_off[nl];
             asm volatile("" ::"s"(wcur), "s"(wnext));
+            const int pi = 1 + 4 * ((step - g.first) * (L + 1) + l);
+            stamp(pi);
             ef_kloop(acc, ring, rW, xs, NS, wcur, wnext, lo, lk, li);
+            stamp(pi + 1);
             // tile c, reg r, lane (lk, li): feature 64w + 4(4lk + r) + c, column li
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -1092,9 +1104,13 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
                     xo[f * NC + li] = gelu_fast(acc[c][r] + bb[c]);
                 }
             }
+            stamp(pi + 2);
             __syncthreads();
+            stamp(pi + 3);
         }
         // head: v[a][j] = sum_k W_L[k][a] h[k][j] + b_L[a]; wave w sums k in [64w, 64w+64)
+        const int ph0 = 1 + 4 * ((step - g.first) * (L + 1) + L);
+        stamp(ph0);
         float* red = slab[L & 1];  // [EF_NW][16 x NC] partial head tiles (this slab is idle now)
         {
             const float* hs = slab[(L - 1) & 1];
@@ -1118,6 +1134,7 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
             *xp = *xp + v / g.steps_f;
         }
         __syncthreads();
+        stamp(ph0 + 3);
     }
     if (tid < A * NC) {
         const int a = tid / NC, j = tid % NC;
@@ -1823,10 +1840,18 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
     const rsrc_t rPart = make_rsrc(gp ? part : g.params, gp ? g.NP : 0);
     const rsrc_t rPe = make_rsrc(P, g.ens);
     // diagnostics only (null unless FQLPOP_PHASE_PROBE): wave 0's view of the phases
+#ifdef FQ_PHASE_PROBE  // diagnostic build only (make PHASE=1)
     unsigned long long* const ph = g.phase != nullptr ? g.phase + (long long)blockIdx.x * SB_PHASE_STRIDE : nullptr;
     auto stamp = [&](int i) {
         if (ph != nullptr && tid == 0) ph[i] = __builtin_amdgcn_s_memrealtime();
     };
+    if (ph != nullptr && tid == 0) {  // where the block ran: HW_ID (CU, SH, SE) and XCC_ID
+        ph[SB_PHASE_STRIDE - 1] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+        ph[SB_PHASE_STRIDE - 2] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
+    }
+#else
+    auto stamp = [](int) {};
+#endif
     stamp(0);
 
 

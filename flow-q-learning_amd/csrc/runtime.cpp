@@ -226,6 +226,9 @@ struct fqlpop {
     unsigned long long* phase_host = nullptr;
     unsigned long long* phase_dev = nullptr;
     long long phase_blocks = 0;
+    unsigned long long* ephase_host = nullptr;  // the same for the persistent Euler launch
+    unsigned long long* ephase_dev = nullptr;
+    long long ephase_blocks = 0;
     int probe_pairs = 0;
     long long probe_blocks = 0;                  // max blocks of one dominant-kernel launch
     int probe_nz[2] = {0, 0};                    // active members of the step that used each set
@@ -862,6 +865,7 @@ EulerArgs euler_args(fqlpop* h, int nz) {
     ea.D = h->D; ea.A = h->A; ea.H = h->H; ea.L = h->L; ea.B = h->B; ea.S = h->S; ea.first = 1;
     ea.steps_f = (float)h->S;
     ea.nz = nz; ea.slots = h->slots;
+    ea.phase = h->ephase_dev;
     return ea;
 }
 
@@ -904,6 +908,40 @@ void phase_report(const unsigned long long* ph, long long nb, int L) {
     for (int i = 0; i < L && i < 8; ++i)
         std::fprintf(stderr, "  pass %d: LN pass 1 %.2f | stats barrier %.2f | pass 2 + du + slab barrier %.2f | dX product %.2f\n",
                      i, pass1[i] * us, wait2[i] * us, p2[i] * us, prod[i] * us);
+}
+
+// FQLPOP_PHASE_PROBE: the persistent Euler launch's mean per-layer phases (us) over its steps
+// and blocks (wave 0's stamps of the last launch)
+void euler_phase_report(const unsigned long long* ph, long long nb, int L, int steps) {
+    double kl[9] = {}, ep[9] = {}, br[9] = {}, gap[9] = {}, pro = 0, blk = 0;
+    long long n = 0;
+    for (long long b = 0; b < nb; ++b) {
+        const unsigned long long* p = ph + b * EF_PHASE_STRIDE;
+        if (p[0] == 0) continue;
+        ++n;
+        pro += (double)(p[1] - p[0]);
+        blk += (double)(p[1 + 4 * ((steps - 1) * (L + 1) + L) + 3] - p[0]);
+        for (int st = 0; st < steps; ++st)
+            for (int l = 0; l <= L; ++l) {
+                const unsigned long long* q = p + 1 + 4 * (st * (L + 1) + l);
+                if (l < L) {
+                    kl[l] += (double)(q[1] - q[0]);
+                    ep[l] += (double)(q[2] - q[1]);
+                    br[l] += (double)(q[3] - q[2]);
+                    gap[l] += (double)(q[0] - (l > 0 ? q[-1] : st > 0 ? q[-1] : q[0]));
+                } else {
+                    kl[l] += (double)(q[3] - q[0]);  // head: MFMAs, reduction, state update
+                }
+            }
+    }
+    if (n == 0) return;
+    const double us = 0.01 / (double)n, per = us / (double)steps;
+    std::fprintf(stderr, "phase probe (Euler flow, last launch): %lld blocks, %d steps, block %.1f us, prologue %.2f us\n",
+                 n, steps, blk * us, pro * us);
+    for (int l = 0; l < L; ++l)
+        std::fprintf(stderr, "  layer %d per step: k-loop %.3f | epilogue %.3f | barrier %.3f | gap before %.3f\n", l,
+                     kl[l] * per, ep[l] * per, br[l] * per, gap[l] * per);
+    std::fprintf(stderr, "  head per step: %.3f\n", kl[L] * per);
 }
 
 // Enqueue one population update (train) or one total_loss pass (!train).
@@ -1443,6 +1481,13 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             HIPCHK(hipHostMalloc((void**)&h->phase_host, phb, hipHostMallocMapped | hipHostMallocCoherent));
             std::memset(h->phase_host, 0, phb);
             HIPCHK(hipHostGetDevicePointer((void**)&h->phase_dev, h->phase_host, 0));
+            if (h->euler_fused && cfg->flow_steps <= 11) {
+                h->ephase_blocks = (long long)(cfg->batch_size / 16) * n_members;
+                const size_t eb = sizeof(unsigned long long) * EF_PHASE_STRIDE * h->ephase_blocks;
+                HIPCHK(hipHostMalloc((void**)&h->ephase_host, eb, hipHostMallocMapped | hipHostMallocCoherent));
+                std::memset(h->ephase_host, 0, eb);
+                HIPCHK(hipHostGetDevicePointer((void**)&h->ephase_dev, h->ephase_host, 0));
+            }
         }
         std::memset(h->probe_host, 0, pb);
         HIPCHK(hipHostGetDevicePointer((void**)&h->probe_slots, h->probe_host, 0));
@@ -1568,8 +1613,18 @@ int fqlpop_destroy(fqlpop_t* h) {
         if (h->probe_host) (void)hipHostFree(h->probe_host);
         if (h->phase_host) {
             (void)hipDeviceSynchronize();
+            if (const char* f = std::getenv("FQLPOP_PHASE_DUMP")) {  // raw stamps for offline analysis
+                if (FILE* fp = std::fopen(f, "wb")) {
+                    std::fwrite(h->phase_host, sizeof(unsigned long long), (size_t)SB_PHASE_STRIDE * h->phase_blocks, fp);
+                    std::fclose(fp);
+                }
+            }
             phase_report(h->phase_host, h->phase_blocks, h->L);
             (void)hipHostFree(h->phase_host);
+        }
+        if (h->ephase_host) {
+            euler_phase_report(h->ephase_host, h->ephase_blocks, h->L, h->S - 1);
+            (void)hipHostFree(h->ephase_host);
         }
         if (h->sX && h->sX != h->sM) (void)hipStreamDestroy(h->sX);
         if (h->sF && h->sF != h->sM) (void)hipStreamDestroy(h->sF);
