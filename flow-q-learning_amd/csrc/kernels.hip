@@ -986,9 +986,12 @@ DEV float gelu_grad_fast(float x) {
 // k < 4 NS (NS a multiple of EF_PF).  ring[] holds the next EF_PF k-steps' A
 // fragments on entry; on exit it holds the first EF_PF of the layer at
 // w_next (element offset of the next layer's Dense kernel).
+// tail >= 0 (layer 0 of the Euler flow): the last pass refills ring[0] from element
+// offset tail (+ lo) instead of the next layer's first k-step; the caller consumes it
+// (ef_tail) and loads the next layer's k-step 0 itself.
 template <int PF = EF_PF>
 DEV void ef_kloop(f32x4 (&acc)[4], float4 (&ring)[PF], rsrc_t rW, const float* xs, int NS, int w_cur,
-                  int w_next, int lo, int lk, int li) {
+                  int w_next, int lo, int lk, int li, int tail = -1) {
     constexpr int H = EF_H, NC = EF_NC;
     float bnext = xs[lk * NC + li];
     // do-while (NS >= PF always): with no zero-trip path the waitcnt pass can prove that
@@ -998,6 +1001,7 @@ DEV void ef_kloop(f32x4 (&acc)[4], float4 (&ring)[PF], rsrc_t rW, const float* x
     do {
         // refill targets: k-steps s0+PF.. of this layer, or the next layer's first PF
         const int rbase = (s0 + PF < NS ? w_cur + 4 * (s0 + PF) * H : w_next) + lo;
+        const int r0 = (s0 + PF >= NS && tail >= 0 ? tail : rbase - lo) + lo;  // ring[0]'s refill
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
             const int s = s0 + p;
@@ -1010,11 +1014,22 @@ DEV void ef_kloop(f32x4 (&acc)[4], float4 (&ring)[PF], rsrc_t rW, const float* x
             acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b, acc[2], 0, 0, 0);
             acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b, acc[3], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            ring[p] = bload4(rW, rbase + 4 * p * H);
+            ring[p] = bload4(rW, p == 0 ? r0 : rbase + 4 * p * H);
             __builtin_amdgcn_sched_barrier(0);
         }
         s0 += PF;
     } while (s0 < NS);
+}
+
+// Layer 0's k-step PF (rows 4 PF .. 4 PF + 3) when the ring pass covered k-steps 0 .. PF-1:
+// a = W[4 PF + lk][64w + 4li .. +3], loaded before the k-loop.
+DEV void ef_tail(f32x4 (&acc)[4], float4 a, const float* xs, int lk, int li) {
+    constexpr int NC = EF_NC;
+    const float b = xs[(4 * EF_PF + lk) * NC + li];
+    acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b, acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b, acc[1], 0, 0, 0);
+    acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b, acc[2], 0, 0, 0);
+    acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b, acc[3], 0, 0, 0);
 }
 
 bool euler_flow_supported(int H, int L, int D, int A, int B) {
@@ -1050,7 +1065,15 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
     stamp(0);
 
     const int D = g.D, A = g.A, L = g.L, B = g.B, S = g.S;
-    const int K0 = D + A + 1, NS0 = (K0 + 4 * PF - 1) / (4 * PF) * PF;  // padded k-steps of layer 0
+    // layer 0's k-steps: K0 <= 4 (PF + 1) runs one ring pass of PF k-steps plus one tail k-step
+    // (ef_tail) instead of 2 PF, of which the padded ones multiply exact zeros
+    const int K0 = D + A + 1;
+#ifdef FQ_NO_EULER_TAIL  // A/B switch
+    const bool tail0 = false;
+#else
+    const bool tail0 = K0 > 4 * PF && K0 <= 4 * (PF + 1);
+#endif
+    const int NS0 = tail0 ? PF : (K0 + 4 * PF - 1) / (4 * PF) * PF;
     const float* __restrict__ P = g.params + (long long)slot * g.P;
     const float* __restrict__ eu = at(g.eu, slot);
     load_in0<NT>(in0, eu, D + A, B, c0);
@@ -1092,7 +1115,15 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
             asm volatile("" ::"s"(wcur), "s"(wnext));
             const int pi = 1 + 4 * ((step - g.first) * (L + 1) + l);
             stamp(pi);
-            ef_kloop(acc, ring, rW, xs, NS, wcur, wnext, lo, lk, li);
+            const bool tl = l == 0 && tail0;
+            // layer 0's tail k-step rides in ring[0] (no extra registers: this kernel's
+            // throughput in the step drops by ~5 % at 107 VGPRs against 101)
+            ef_kloop(acc, ring, rW, xs, NS, wcur, wnext, lo, lk, li, tl ? wcur + 4 * PF * H : -1);
+            if (tl) {
+                ef_tail(acc, ring[0], xs, lk, li);
+                __builtin_amdgcn_sched_barrier(0);
+                ring[0] = bload4(rW, wnext + lo);
+            }
             stamp(pi + 1);
             // tile c, reg r, lane (lk, li): feature 64w + 4(4lk + r) + c, column li
 #pragma unroll
@@ -1367,7 +1398,8 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
     const int L = g.L, K0 = g.K0, nout = g.head.nout;
-    const int NS0 = (K0 + 4 * PF - 1) / (4 * PF) * PF;
+    const bool tail0 = K0 > 4 * PF && K0 <= 4 * (PF + 1);  // layer 0 as in euler_flow_kernel
+    const int NS0 = tail0 ? PF : (K0 + 4 * PF - 1) / (4 * PF) * PF;
     const float* __restrict__ P = g.params + (long long)slot * g.P + (long long)y * g.ens;
     const float* __restrict__ x0 = g.x0 + (long long)slot * g.x0_ss;
     load_in0<NT>(in0, x0, K0, g.ld_x, c0);
@@ -1404,7 +1436,9 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
         const float pe = LN ? P[g.be_off[lp] + tid] : 0.f;
         const int wcur = (int)g.w_off[l], wnext = (int)g.w_off[nl];
         asm volatile("" ::"s"(wcur), "s"(wnext));  // no SMEM load in flight into the k-loop (see euler_flow_kernel)
+        const float4 at0 = bload4(rW, wcur + 4 * PF * H + lo);  // layer 0's tail k-step (l > 0: unused)
         ef_kloop(acc, ring, rW, xs, NS, wcur, wnext, lo, lk, li);
+        if (l == 0 && tail0) ef_tail(acc, at0, xs, lk, li);
         if constexpr (!LN) {
             lnp[0][tid] = pb;
             __syncthreads();  // every wave is done reading the slab; lnp visible
