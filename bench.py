@@ -285,7 +285,9 @@ def main():
     if os.path.exists(args.pmc_json):
         with open(args.pmc_json) as f:
             pmc = json.load(f)
-        if pmc.get("kernel_regex") and pmc["kernel_regex"] in kname and pmc.get("members") == pop.n:
+        # the counters were collected on one workload's launch (pmc_dominant.json "workload")
+        if (pmc.get("kernel_regex") and pmc["kernel_regex"] in kname and pmc.get("members") == pop.n
+                and pmc.get("workload", "cube") == args.workload):
             traffic = pmc["traffic_bytes_per_launch"]
 
     result = {
