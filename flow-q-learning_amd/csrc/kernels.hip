@@ -2722,7 +2722,8 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void rollout_kernel(const RolloutArg
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
     const int D = g.D, A = g.A, L = g.L, K0 = D + A;
-    const int NS0 = (K0 + 4 * PF - 1) / (4 * PF) * PF;
+    const bool tail0 = K0 > 4 * PF && K0 <= 4 * (PF + 1);  // layer 0 as in euler_flow_kernel
+    const int NS0 = tail0 ? PF : (K0 + 4 * PF - 1) / (4 * PF) * PF;
     const float* __restrict__ P = g.params + (long long)slot * g.P + g.os_off;
     const uint64_t key = g.seed ^ (g.member_seeds[slot] * 0x9E3779B97F4A7C15ull);
 
@@ -2791,7 +2792,14 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void rollout_kernel(const RolloutArg
             float4 bias4[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) bias4[r] = bload4(rW, (int)g.b_off[l] + 64 * w + 16 * lk + 4 * r);
-            ef_kloop(acc, ring, rW, xs, NS, (int)g.w_off[l], (int)g.w_off[nl], lo, lk, li);
+            const bool tl = l == 0 && tail0;
+            ef_kloop(acc, ring, rW, xs, NS, (int)g.w_off[l], (int)g.w_off[nl], lo, lk, li,
+                     tl ? (int)g.w_off[0] + 4 * PF * H : -1);
+            if (tl) {
+                ef_tail(acc, ring[0], xs, lk, li);
+                __builtin_amdgcn_sched_barrier(0);
+                ring[0] = bload4(rW, (int)g.w_off[nl] + lo);
+            }
             __syncthreads();  // every wave done reading the slab
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
