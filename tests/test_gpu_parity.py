@@ -25,8 +25,8 @@ def _cfgs(H, B, alpha, **kw):
 
 def _pop(H, B, alphas, seeds, use_graph=True, **kw):
     from fqlpop import Population, PopulationConfig
-    pc = PopulationConfig(obs_dim=28, action_dim=5, hidden_dims=(H,) * 4, batch_size=B,
-                          use_graph=use_graph, **kw)
+    kw = {"obs_dim": 28, "action_dim": 5, **kw}
+    pc = PopulationConfig(hidden_dims=(H,) * 4, batch_size=B, use_graph=use_graph, **kw)
     return Population(pc, alphas, seeds)
 
 
@@ -113,6 +113,15 @@ def test_update_parity_q_min_normalized():
 ])
 def test_update_parity_configs(H, B, kw):
     _run_parity(H, B, [4.0, 40.0], n_steps=2, **kw)
+
+
+@pytest.mark.parametrize("D,A", [(26, 5), (27, 5), (30, 5), (31, 5)])
+def test_update_parity_layer0_widths(D, A):
+    """Layer-0 widths around the streamed kernels' k-step split (one ring pass of 8 k-steps =
+    32 input rows, plus one tail k-step up to 36 rows; wider inputs run two ring passes):
+    the Euler / BC input is K0 = D + A + 1 rows (32, 33, 36, 37 here), the critic's and the
+    one-step actor's K0 = D + A (31, 32, 35, 36)."""
+    _run_parity(512, 64, [7.0], n_steps=1, obs_dim=D, action_dim=A)
 
 
 def test_update_parity_ant_full_size():
