@@ -1094,8 +1094,10 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
     __syncthreads();
 
     for (int step = g.first; step < S; ++step) {
-        if (tid < NC) in0[(D + A) * NC + tid] = (float)((double)step / (double)S);
-        __syncthreads();
+        if (step == g.first) {  // later steps' time rows are written with the x update
+            if (tid < NC) in0[(D + A) * NC + tid] = (float)((double)step / (double)S);
+            __syncthreads();
+        }
         for (int l = 0; l < L; ++l) {
             const int NS = l == 0 ? NS0 : H / 4;
             const float* xs = l == 0 ? in0 : slab[(l - 1) & 1];
@@ -1163,6 +1165,8 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void euler_flow_kernel(const EulerAr
             v += b5s[a];
             float* xp = &in0[(D + a) * NC + j];
             *xp = *xp + v / g.steps_f;
+        } else if (tid < (A + 1) * NC && step + 1 < S) {  // the next step's time row
+            in0[(D + A) * NC + tid - A * NC] = (float)((double)(step + 1) / (double)S);
         }
         __syncthreads();
         stamp(ph0 + 3);
