@@ -10,6 +10,13 @@ grad-steps per second over all ranks (weak scaling: 16 members per GPU).
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py is its own
+launcher: the parent (which makes no GPU call) starts N rank processes with
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rank r on cuda:r over RCCL, and
+exits with the first failing rank's status.  --share-device puts every rank on
+cuda:0 over gloo (a rehearsal of the N-rank path on a one-GPU box).  A world size
+that differs from --gpus is an error.
+
 Rank 0 prints ONE JSON line.  Data is synthetic (no network): 1M transitions,
 obs ~ N(0,1), act ~ U(-1+1e-5, 1-1e-5), next_obs = obs + 0.05 N(0,1),
 reward in {-1, 0} with P(0) = 0.05, mask = 1 - (reward == 0).
@@ -18,9 +25,10 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import random
+import socket
+import subprocess
 import sys
 import time
 
@@ -64,6 +72,75 @@ def population_values(n_total: int, seed: int = 0):
     return alphas, seeds
 
 
+def host_cpu() -> dict:
+    """Host core counts and CPU model (cpu_baseline labels)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = None
+    return {"os_cpu_count": os.cpu_count(), "affinity_cpus": allowed, "model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def _pci_sysfs(device_index: int):
+    """sysfs directory of the PCI function behind cuda:<device_index> (None if unknown).
+    torch.cuda.get_device_properties only reads the already-initialised device table."""
+    try:
+        pr = torch.cuda.get_device_properties(device_index)
+        addr = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+    except Exception:
+        return None
+    d = os.path.join("/sys/bus/pci/devices", addr)
+    return d if os.path.isdir(d) else None
+
+
+def gpu_clock_power(device_index: int) -> dict:
+    """Current shader clock (MHz), power (W) and power cap (W) of the GPU from sysfs /
+    hwmon: microsecond reads, so the timed region's edges stay busy-clocked.  Values the
+    box does not expose are null."""
+    out = {"sclk_mhz": None, "power_w": None, "power_cap_w": None}
+    d = _pci_sysfs(device_index)
+    if d is None:
+        out["error"] = "no sysfs PCI node for the device"
+        return out
+
+    def rd(path):
+        try:
+            with open(path) as f:
+                return f.read()
+        except OSError:
+            return None
+
+    txt = rd(os.path.join(d, "pp_dpm_sclk"))
+    if txt:
+        for line in txt.splitlines():
+            if line.strip().endswith("*"):
+                try:
+                    out["sclk_mhz"] = int(line.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz"))
+                except (IndexError, ValueError):
+                    pass
+    hw_root = os.path.join(d, "hwmon")
+    for hw in sorted(os.listdir(hw_root)) if os.path.isdir(hw_root) else []:
+        base = os.path.join(hw_root, hw)
+        f = rd(os.path.join(base, "freq1_input"))
+        if out["sclk_mhz"] is None and f and f.strip().isdigit():
+            out["sclk_mhz"] = int(f) // 1_000_000
+        for key, name in (("power_w", "power1_average"), ("power_w", "power1_input"), ("power_cap_w", "power1_cap")):
+            v = rd(os.path.join(base, name))
+            if out[key] is None and v and v.strip().isdigit():
+                out[key] = round(int(v) / 1e6, 1)
+    return out
+
+
 def cpu_baseline(wl: dict, data: dict, budget_s: float, threads: int) -> dict:
     """The oracle's float32 PyTorch-CPU restatement (kind "port") of one member's
     update on the same synthetic data, timed on this host's cores."""
@@ -92,9 +169,14 @@ def cpu_baseline(wl: dict, data: dict, budget_s: float, threads: int) -> dict:
         el = time.perf_counter() - t0
         if el >= budget_s and steps >= 3:
             break
+    host = host_cpu()
     return {"value": steps / el, "unit": "member-grad-steps/s", "cores": threads, "kind": "port",
+            "host": host,
             "sample": f"{steps} sequential update() steps of 1 member (alpha=10, B={B}, H=512) in {el:.1f} s, "
-                      f"float32 PyTorch-CPU restatement (oracle/fql_torch.py), torch threads={threads}"}
+                      f"float32 PyTorch-CPU restatement (oracle/fql_torch.py), torch threads={threads} = the "
+                      f"CPUs this job may use (sched_getaffinity {host['affinity_cpus']}, OMP_NUM_THREADS "
+                      f"{host['omp_num_threads']}); os.cpu_count() {host['os_cpu_count']} counts the whole host. "
+                      f"BASELINE C1 (1k steps) at this rate: {1000.0 * el / steps:.0f} s"}
 
 
 def eval_rollout_leg(pop, wl: dict, n_envs: int, steps: int, dev) -> dict:
@@ -171,7 +253,39 @@ def envmodel_train_leg(wl: dict, data: dict, steps: int) -> dict:
     return out
 
 
-def main():
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list) -> int:
+    """Launcher for ``--gpus N`` without torch.distributed.run: N fresh rank processes
+    (this parent makes no GPU call), rank r -> LOCAL_RANK r.  Rank 0 prints the JSON
+    line.  If a rank fails, the others are terminated and its status is returned."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log(f"bench.py: rank process {p.pid} exited with {code}; stopping the others")
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.1)
+    return rc
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
@@ -195,23 +309,52 @@ def main():
     ap.add_argument("--eval-steps", type=int, default=1000, help="world-model rollout leg: max_episode_steps")
     ap.add_argument("--envmodel-train-steps", type=int, default=2000,
                     help="env-model training leg: train_steps per model (0 disables the leg)")
-    args = ap.parse_args()
+    ap.add_argument("--share-device", action="store_true",
+                    help="every rank on cuda:0 over gloo (rehearse the N-rank path on one GPU)")
+    ap.add_argument("--serial", action="store_true",
+                    help="profiling: every launch of the step on one stream (engine option serial)")
+    ap.add_argument("--diagnostic", action="store_true",
+                    help="allow FQLPOP_* environment variables (developer A/B runs); they are recorded")
+    args = ap.parse_args(argv)
 
+    fq_env = {k: v for k, v in os.environ.items() if k.startswith("FQLPOP_")}
+    if fq_env and not args.diagnostic:
+        log(f"bench.py: refusing to measure with {sorted(fq_env)} set (developer switches); "
+            "unset them or pass --diagnostic")
+        return 2
+    if args.gpus < 1:
+        log("bench.py: --gpus must be >= 1")
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:] if argv is None else list(argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench.py: world size {world} (WORLD_SIZE) != --gpus {args.gpus}")
+        return 2
     distributed = world > 1
-    torch.cuda.set_device(local_rank)
+    if not args.share_device and torch.cuda.device_count() < world:  # device_count: no GPU init
+        log(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPU(s); --share-device "
+            "rehearses the N-rank path on one GPU")
+        return 2
+    dev_index = 0 if args.share_device else local_rank
+    torch.cuda.set_device(dev_index)
     if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.share_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
 
-    from fqlpop import Population, PopulationConfig
+    from fqlpop import Population, PopulationConfig, set_engine_option
+    if args.serial:
+        set_engine_option("serial", 1)
 
     wl = WORKLOADS[args.workload]
     # dataset: generated on rank 0, broadcast over RCCL (xGMI) to every rank
     from fqlpop import distributed as D
     data = synthetic_dataset(args.rows, wl["obs_dim"], wl["action_dim"]) if rank == 0 else None
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", dev_index)
     shapes = {"observations": (args.rows, wl["obs_dim"]), "actions": (args.rows, wl["action_dim"]),
               "rewards": (args.rows,), "masks": (args.rows,), "next_observations": (args.rows, wl["obs_dim"])}
     dev_data = D.broadcast_dataset(data, shapes, dev)
@@ -221,7 +364,7 @@ def main():
     alphas, seeds = D.shard(alphas_all, rank, world), D.shard(seeds_all, rank, world)
     pcfg = PopulationConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"], batch_size=wl["batch_size"],
                             use_graph=not args.no_graph)
-    pop = Population(pcfg, alphas, seeds, device=local_rank)
+    pop = Population(pcfg, alphas, seeds, device=dev_index)
     pop.set_dataset(dev_data)
     del dev_data
     torch.cuda.empty_cache()
@@ -252,6 +395,7 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
+    clk0 = gpu_clock_power(dev_index)
     t0 = time.perf_counter()
     chunk = max(1, min(100, args.steps))
     done = 0
@@ -259,12 +403,13 @@ def main():
         k = min(chunk, args.steps - done)
         pop.step(k)
         done += k
+    clk1 = gpu_clock_power(dev_index)  # the last chunk is still running: the loaded clock
     pop.sync()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if distributed:
         dist.barrier()
-    el = D.max_over_ranks(el, dev)
+    el = D.max_over_ranks(el, None if args.share_device else dev)
     probe_us, probe_n, _ = pop.read_probe()
     pop.set_probe(False)
     info = pop.read_info_array()
@@ -316,7 +461,12 @@ def main():
             "parallelism": f"weak: {args.members} members per GPU x {world} GPU(s), no data-path collective",
             "graph": not args.no_graph,
             "info_finite": finite,
+            "share_device": bool(args.share_device),
+            "serial_streams": bool(args.serial),
         },
+        "gpu_clock": {"device": torch.cuda.get_device_name(dev_index), "start": clk0, "end": clk1,
+                      "note": "sysfs pp_dpm_sclk / hwmon of this rank's GPU, read just before the clock "
+                              "starts and before the final synchronize (GPU still busy)"},
         "roofline": {
             "bound": "mfma",
             "kernel": kname + (" (Euler flow steps 1..9 of all members: 16-column blocks, weights streamed, "
@@ -348,13 +498,16 @@ def main():
         threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
         log(f"[rank 0] cpu baseline ({args.cpu_baseline_seconds:.0f} s budget, {threads} threads)")
         result["cpu_baseline"] = cpu_baseline(wl, data, args.cpu_baseline_seconds, threads)
+    if fq_env:
+        result["diagnostic_env"] = fq_env
     if rank == 0:
         print(json.dumps(result), flush=True)
     pop.close()
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

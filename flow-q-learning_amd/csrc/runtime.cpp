@@ -52,6 +52,49 @@ struct FqErr {
 constexpr long long kAlign = 64;  // floats (256 B)
 long long align_up(long long x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
+// Timing-only switches that change or corrupt results (launches left out, phases of the
+// fused optimiser switched off, cross-step pipelining without the step's joins, per-block
+// phase stamps) exist only in the diagnostic builds (make DIAG=1 / PHASE=1, -DFQ_DIAG).
+// The production library reads no environment variable at all: diag_env is nullptr.
+#ifdef FQ_DIAG
+const char* diag_env(const char* name) { return std::getenv(name); }
+#else
+const char* diag_env(const char*) { return nullptr; }
+#endif
+
+// Engine options (fqlpop_set_engine_option): alternate code paths and stream schedules
+// that give the same results (bit-identical, or the per-layer / unfused paths within the
+// parity tolerance), read by fqlpop_create.  Test and profiling hooks; the defaults are the
+// measured-fastest configuration (DESIGN.md sections 4-5).
+struct EngineOptions {
+    int euler_fused = 1;   // persistent Euler launch (0: per-layer GEMMs)
+    int stream_fwd = 1;    // whole-network forward launches
+    int stream_bwd = 1;    // whole-network dX chains
+    int fused_adam = 1;    // optimiser in the grouped dW epilogue
+    int cdw_sb = 1;        // critic dW + optimiser on the BC stream, beside the actor chain
+    int serial = 0;        // every launch on one stream (uncontended kernel traces)
+    int streams = 3;       // 4: target critic + dW/optimiser on a 4th stream
+    int prio = 0;          // stream priorities: 1 main chain high, 2 flow high
+    int dw_tile_critic = 10, dw_tile_actor = 10;  // grouped dW tile ids (launch_gemm_group_dw)
+    int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
+};
+EngineOptions g_engine_opts;
+
+struct EngineOptionRef {
+    const char* name;
+    int EngineOptions::*field;
+    int lo, hi;
+};
+const EngineOptionRef kEngineOptions[] = {
+    {"euler_fused", &EngineOptions::euler_fused, 0, 1}, {"stream_fwd", &EngineOptions::stream_fwd, 0, 1},
+    {"stream_bwd", &EngineOptions::stream_bwd, 0, 1},   {"fused_adam", &EngineOptions::fused_adam, 0, 1},
+    {"cdw_sb", &EngineOptions::cdw_sb, 0, 1},           {"serial", &EngineOptions::serial, 0, 1},
+    {"streams", &EngineOptions::streams, 3, 4},         {"prio", &EngineOptions::prio, 0, 2},
+    {"dw_tile_critic", &EngineOptions::dw_tile_critic, 0, 10},
+    {"dw_tile_actor", &EngineOptions::dw_tile_actor, 0, 10},
+    {"adam_nt", &EngineOptions::adam_nt, 0, 3},
+};
+
 // ---------------------------------------------------------------- host Philox
 void philox_host(uint32_t c[4], uint32_t k0, uint32_t k1) {
     for (int r = 0; r < 10; ++r) {
@@ -131,6 +174,7 @@ struct Graphs {
 
 struct fqlpop {
     fqlpop_config cfg{};
+    EngineOptions opt{};  // g_engine_opts at create
     int n = 0;          // slots
     int device = 0;
     int D = 0, A = 0, H = 0, L = 0, B = 0, E = 0, S = 0;
@@ -317,11 +361,9 @@ long long leaf_member_size(const NetLayout& N, int kind, int layer) {
 // overlap one block's HBM-bound epilogue with the others' k-loops better than
 // 2 blocks of 128 x 128.  BK = 16: 33 KB of LDS and 129 VGPRs instead of 51 KB and
 // 146, +0.6 % same-box; 10 = the same at <= 128 VGPRs, 4 blocks per CU instead of 3,
-// +0.4 % same-box; FQLPOP_DW_TILE_C / _A override, for measurements)
-int dw_tile(const NetLayout& N) {
-    const char* t = std::getenv(N.E > 1 ? "FQLPOP_DW_TILE_C" : "FQLPOP_DW_TILE_A");
-    if (t) return std::atoi(t);
-    return 10;
+// +0.4 % same-box; engine options dw_tile_critic / dw_tile_actor override, for measurements)
+int dw_tile(const fqlpop* h, const NetLayout& N) {
+    return N.E > 1 ? h->opt.dw_tile_critic : h->opt.dw_tile_actor;
 }
 
 void build_chunks(fqlpop* h) {
@@ -340,7 +382,7 @@ void build_chunks(fqlpop* h) {
                 if (h->fused_adam && kind == 0 && l < N.L) {
                     // W_l: the fused dW epilogue writes one stats chunk per tile
                     h->w_stat_base[ni][l] = (int)all.size();
-                    const int nt = gemm_group_tiles(dw_tile(N), N.kdim(l), N.H) * N.E;
+                    const int nt = gemm_group_tiles(dw_tile(h, N), N.kdim(l), N.H) * N.E;
                     for (int t = 0; t < nt; ++t) {
                         all.push_back(Chunk{0, 0, leaf_id});
                         all_leaf.push_back(leaf_id);
@@ -716,20 +758,21 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         ae.count = h->count;
         ae.lr = h->cfg.lr; ae.tau = h->cfg.tau;
         {
-            const char* dm = std::getenv("FQLPOP_DW_MODE");
+            // FQLPOP_DW_MODE (diagnostic builds only, timing probes with wrong results):
+            // 1 / 2 one phase of the launch, 3 no W^T pass, 4 no W^T pass for the actor nets
+            const char* dm = diag_env("FQLPOP_DW_MODE");
             ae.mode = dm ? std::atoi(dm) : 0;
-            if (ae.mode == 4) ae.mode = ni == 0 ? 0 : 3;  // timing probe: no W^T pass for the actor nets
+            if (ae.mode == 4) ae.mode = ni == 0 ? 0 : 3;
             // m, v and the target stream non-temporally: read and written once per step, they
             // need not displace the weights the streamed kernels re-read from L2 / MALL
-            // (+1.0 % same-box; FQLPOP_ADAM_NT: bit mask, see AdamEpi::nt)
-            const char* nt = std::getenv("FQLPOP_ADAM_NT");
-            ae.nt = nt ? std::atoi(nt) : 3;
+            // (+1.0 % same-box; engine option adam_nt: bit mask, see AdamEpi::nt)
+            ae.nt = h->opt.adam_nt;
         }
         ae.small = adam_args(c, ni);
         ae.small_blocks = ae.small.n_chunks * c.nz;
-        launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw, &ae);
+        launch_gemm_group_dw(dw_tile(h, N), gs.data(), (int)gs.size(), sw, &ae);
     } else if (N.L <= GEMM_GROUP_MAX && N.H % 128 == 0) {
-        launch_gemm_group_dw(dw_tile(N), gs.data(), (int)gs.size(), sw);
+        launch_gemm_group_dw(dw_tile(h, N), gs.data(), (int)gs.size(), sw);
     } else {
         for (const GemmArgs& gw : gs) gemm(LAYOUT_DW, EPI_STORE, gw, sw);
     }
@@ -840,12 +883,12 @@ void stream_fwd(const Ctx& c, hipStream_t s, const NetLayout& N, const float* ar
     if (!(sk & bit)) launch_stream_fwd(mode, N.ln, a, s);
 }
 
-// FQLPOP_SKIP (TIMING EXPERIMENT ONLY, results are garbage): bit mask of launches left
-// out of the step, to measure each one's marginal cost in the concurrent step:
-// 1 Euler flow, 2 target-critic fwd, 4 critic fwd, 8 one-step fwd, 16 BC fwd,
-// 32 critic bwd (dX chain), 64 BC bwd, 128 one-step bwd
+// FQLPOP_SKIP (diagnostic builds only; TIMING EXPERIMENT, results are garbage): bit mask
+// of launches left out of the step, to measure each one's marginal cost in the concurrent
+// step: 1 Euler flow, 2 target-critic fwd, 4 critic fwd, 8 one-step fwd, 16 BC fwd,
+// 32 critic bwd (dX chain), 64 BC bwd, 128 one-step bwd.  Always 0 in the production build.
 int skip_mask() {
-    static const int m = [] { const char* v = std::getenv("FQLPOP_SKIP"); return v ? std::atoi(v) : 0; }();
+    static const int m = [] { const char* v = diag_env("FQLPOP_SKIP"); return v ? std::atoi(v) : 0; }();
     return m;
 }
 
@@ -1354,6 +1397,43 @@ extern "C" {
 
 const char* fqlpop_last_error(void) { return g_err.c_str(); }
 
+int fqlpop_set_engine_option(const char* name, int value) {
+    return guard([&] {
+        ARGCHK(name != nullptr, "null option name");
+        for (const EngineOptionRef& o : kEngineOptions)
+            if (std::strcmp(o.name, name) == 0) {
+                ARGCHK(value >= o.lo && value <= o.hi, std::string("engine option ") + name + " out of range");
+                g_engine_opts.*o.field = value;
+                return;
+            }
+        throw FqErr{FQLPOP_E_ARG, std::string("unknown engine option ") + name};
+    });
+}
+
+int fqlpop_get_engine_option(const char* name, int* value) {
+    return guard([&] {
+        ARGCHK(name != nullptr && value != nullptr, "null argument");
+        for (const EngineOptionRef& o : kEngineOptions)
+            if (std::strcmp(o.name, name) == 0) {
+                *value = g_engine_opts.*o.field;
+                return;
+            }
+        throw FqErr{FQLPOP_E_ARG, std::string("unknown engine option ") + name};
+    });
+}
+
+int fqlpop_reset_engine_options(void) {
+    return guard([&] { g_engine_opts = EngineOptions{}; });
+}
+
+int fqlpop_diagnostic_build(void) {
+#ifdef FQ_DIAG
+    return 1;
+#else
+    return 0;
+#endif
+}
+
 double fqlpop_flops_per_member_step(const fqlpop_config* c) {
     // F(i,o) = 2B(iH + (L-1)H^2 + Ho) per forward; dX without
     // the first layer = 2B((L-1)H^2 + Ho).
@@ -1402,33 +1482,25 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         h->PT = align_up(h->critic.size());
         build_leaves(h.get());
 
-        // Stream priorities (FQLPOP_PRIO, experiment switch): 0 = all default
-        // (measured fastest), 1 = main chain high, 2 = Euler flow high.
+        h->opt = g_engine_opts;
+        const EngineOptions& eo = h->opt;
+        // Stream priorities (engine option prio): 0 = all default (measured fastest),
+        // 1 = main chain high, 2 = Euler flow high.
         {
             int least = 0, greatest = 0;
             HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-            const char* pe = std::getenv("FQLPOP_PRIO");
-            const int mode = pe ? std::atoi(pe) : 0;
-            HIPCHK(hipStreamCreateWithPriority(&h->sM, hipStreamNonBlocking, mode == 1 ? greatest : 0));
-            HIPCHK(hipStreamCreateWithPriority(&h->sF, hipStreamNonBlocking, mode == 2 ? greatest : 0));
-            HIPCHK(hipStreamCreateWithPriority(&h->sB, hipStreamNonBlocking, mode == 1 ? least : 0));
-        }
-        // FQLPOP_SERIAL=1 (profiling switch): every kernel of the step on sM, so a
-        // kernel trace shows uncontended durations
-        bool serial = false;
-        {
-            const char* se = std::getenv("FQLPOP_SERIAL");
-            serial = se && std::atoi(se) == 1;
+            HIPCHK(hipStreamCreateWithPriority(&h->sM, hipStreamNonBlocking, eo.prio == 1 ? greatest : 0));
+            HIPCHK(hipStreamCreateWithPriority(&h->sF, hipStreamNonBlocking, eo.prio == 2 ? greatest : 0));
+            HIPCHK(hipStreamCreateWithPriority(&h->sB, hipStreamNonBlocking, eo.prio == 1 ? least : 0));
         }
         // A 4th stream (target critic + dW GEMMs + Adams off the main chain) is
         // opt-in: on MI355X the step is throughput-bound and the extra
         // concurrency measured 5% slower.
-        {
-            const char* ns = std::getenv("FQLPOP_STREAMS");
-            if (ns && std::atoi(ns) >= 4) HIPCHK(hipStreamCreateWithFlags(&h->sX, hipStreamNonBlocking));
-            else h->sX = h->sM;
-        }
-        if (serial) {
+        if (eo.streams >= 4) HIPCHK(hipStreamCreateWithFlags(&h->sX, hipStreamNonBlocking));
+        else h->sX = h->sM;
+        // serial (profiling option): every kernel of the step on sM, so a kernel trace
+        // shows uncontended durations
+        if (eo.serial) {
             HIPCHK(hipStreamDestroy(h->sF));
             HIPCHK(hipStreamDestroy(h->sB));
             if (h->sX != h->sM) HIPCHK(hipStreamDestroy(h->sX));
@@ -1436,34 +1508,19 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         }
         h->ev_pool.resize(64);
         {
-            const char* pe = std::getenv("FQLPOP_PIPE_EXP");
+            // FQLPOP_PIPE_EXP (diagnostic builds only; eager launches, racy): the next step's
+            // sampling / BC forward / flow start before the previous step has finished
+            const char* pe = diag_env("FQLPOP_PIPE_EXP");
             h->pipe_exp = pe && !cfg->use_graph ? std::atoi(pe) : 0;
         }
-        {
-            const char* ef = std::getenv("FQLPOP_EULER");
-            h->euler_fused = euler_flow_supported(H, L, D, A, B) && !h->bc.ln && !(ef && std::atoi(ef) == 0);
-        }
-        {
-            const char* sf = std::getenv("FQLPOP_STREAM");
-            h->stream_fwd = stream_fwd_supported(H, L, D + A + 1, A, B) && !(sf && std::atoi(sf) == 0);
-        }
-        {
-            const char* sb = std::getenv("FQLPOP_SBWD");
-            h->stream_bwd = stream_bwd_supported(H, L, A, B, B) &&
-                            !(sb && std::atoi(sb) == 0);
-        }
-        {
-            // the critic's fused dW + optimiser on the BC stream (idle by then), beside the
-            // actor chain: +0.5-0.9 % (FQLPOP_CDW_SB=0: on the main chain's queue)
-            const char* cs = std::getenv("FQLPOP_CDW_SB");
-            h->cdw_sb = !(cs && std::atoi(cs) == 0);
-        }
-        {
-            // Adam / EMA / W^T / grad stats fused into the grouped dW epilogue
-            const char* fa = std::getenv("FQLPOP_FUSED_ADAM");
-            h->fused_adam = h->stream_bwd && H % 128 == 0 && L <= GEMM_GROUP_MAX && h->critic.off == 0 &&
-                            !(fa && std::atoi(fa) == 0);
-        }
+        h->euler_fused = euler_flow_supported(H, L, D, A, B) && !h->bc.ln && eo.euler_fused;
+        h->stream_fwd = stream_fwd_supported(H, L, D + A + 1, A, B) && eo.stream_fwd;
+        h->stream_bwd = stream_bwd_supported(H, L, A, B, B) && eo.stream_bwd;
+        // the critic's fused dW + optimiser on the BC stream (idle by then), beside the
+        // actor chain: +0.5-0.9 % (cdw_sb = 0: on the main chain's queue)
+        h->cdw_sb = eo.cdw_sb != 0;
+        // Adam / EMA / W^T / grad stats fused into the grouped dW epilogue
+        h->fused_adam = h->stream_bwd && H % 128 == 0 && L <= GEMM_GROUP_MAX && h->critic.off == 0 && eo.fused_adam;
         if (h->euler_fused) {  // dominant kernel: one persistent Euler launch per step
             h->probe_pairs = 1;
             h->probe_blocks = (long long)(cfg->batch_size / 16) * n_members;
@@ -1475,8 +1532,10 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         // event, with no device-to-host copy (a copy kernel) interleaved with the steps
         const size_t pb = sizeof(unsigned long long) * 4 * h->probe_blocks * h->probe_pairs;
         HIPCHK(hipHostMalloc((void**)&h->probe_host, pb, hipHostMallocMapped | hipHostMallocCoherent));
-        if (const char* e = std::getenv("FQLPOP_PHASE_PROBE"); e != nullptr && e[0] == '1') {
-            h->phase_blocks = (long long)(2 * cfg->batch_size / 16) * 2 * n_members;  // critic: 2B columns, 2 members
+#ifdef FQ_PHASE_PROBE  // the kernels write the phase stamps only in this build (make PHASE=1)
+        if (const char* e = diag_env("FQLPOP_PHASE_PROBE"); e != nullptr && e[0] == '1') {
+            // the critic backward's blocks: 2B columns in 16-column tiles per ensemble member
+            h->phase_blocks = (long long)(2 * cfg->batch_size / 16) * E * n_members;
             const size_t phb = sizeof(unsigned long long) * SB_PHASE_STRIDE * h->phase_blocks;
             HIPCHK(hipHostMalloc((void**)&h->phase_host, phb, hipHostMallocMapped | hipHostMallocCoherent));
             std::memset(h->phase_host, 0, phb);
@@ -1489,6 +1548,7 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
                 HIPCHK(hipHostGetDevicePointer((void**)&h->ephase_dev, h->ephase_host, 0));
             }
         }
+#endif
         std::memset(h->probe_host, 0, pb);
         HIPCHK(hipHostGetDevicePointer((void**)&h->probe_slots, h->probe_host, 0));
         for (auto& e : h->probe_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1613,7 +1673,7 @@ int fqlpop_destroy(fqlpop_t* h) {
         if (h->probe_host) (void)hipHostFree(h->probe_host);
         if (h->phase_host) {
             (void)hipDeviceSynchronize();
-            if (const char* f = std::getenv("FQLPOP_PHASE_DUMP")) {  // raw stamps for offline analysis
+            if (const char* f = diag_env("FQLPOP_PHASE_DUMP")) {  // raw stamps for offline analysis
                 if (FILE* fp = std::fopen(f, "wb")) {
                     std::fwrite(h->phase_host, sizeof(unsigned long long), (size_t)SB_PHASE_STRIDE * h->phase_blocks, fp);
                     std::fclose(fp);

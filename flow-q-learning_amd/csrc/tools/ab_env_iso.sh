@@ -8,7 +8,7 @@ cd "$R"
 for rep in 1 2; do
   for spec in "$@"; do
     envs=${spec%%|*}; args=${spec#*|}
-    env $envs timeout -k 5 120 python bench.py --steps 400 --no-cpu-baseline --no-probe --eval-envs 0 \
+    env $envs timeout -k 5 120 python bench.py --diagnostic --steps 400 --no-cpu-baseline --no-probe --eval-envs 0 \
         --envmodel-train-steps 0 --kernel-iters 20 $args 2>/dev/null \
       | python -c "import json,sys; d=json.load(sys.stdin); print('[$envs|$args]', d['value'], d['ms_per_step'], 'iso_us', d['roofline']['isolated_launch_us'])" || exit 1
   done

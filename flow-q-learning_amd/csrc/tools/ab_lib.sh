@@ -8,6 +8,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 for f in new ref new ref new ref; do
     if [ $f = ref ]; then export FQLPOP_LIB=$R/flow-q-learning_amd/fqlpop/libfqlpop_ref.so; else unset FQLPOP_LIB; fi
-    timeout -k 5 120 python bench.py --steps 400 --no-cpu-baseline --no-probe --eval-envs 0 --envmodel-train-steps 0 "$@" \
+    timeout -k 5 120 python bench.py --diagnostic --steps 400 --no-cpu-baseline --no-probe --eval-envs 0 --envmodel-train-steps 0 "$@" \
         2>/dev/null | python -c "import json,sys; d=json.load(sys.stdin); print('$f', d['value'], d['ms_per_step'])" || exit 1
 done

@@ -9,7 +9,7 @@ cd "$R"
 for rep in 1 2; do
   for f in "$@"; do
     if [ "$f" = new ]; then unset FQLPOP_LIB; else export FQLPOP_LIB=$R/flow-q-learning_amd/fqlpop/libfqlpop_$f.so; fi
-    timeout -k 5 120 python bench.py --steps 400 --no-cpu-baseline --no-probe --eval-envs 0 --envmodel-train-steps 0 \
+    timeout -k 5 120 python bench.py --diagnostic --steps 400 --no-cpu-baseline --no-probe --eval-envs 0 --envmodel-train-steps 0 \
         2>/dev/null | python -c "import json,sys; d=json.load(sys.stdin); print('$f', d['value'], d['ms_per_step'])" || exit 1
   done
 done

@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 for rep in 1 2 3; do
   for p in "" "--no-probe"; do
-    timeout -k 5 120 python bench.py --steps 400 --no-cpu-baseline --eval-envs 0 --envmodel-train-steps 0 $p "$@" \
+    timeout -k 5 120 python bench.py --diagnostic --steps 400 --no-cpu-baseline --eval-envs 0 --envmodel-train-steps 0 $p "$@" \
         2>/dev/null | python -c "import json,sys; d=json.load(sys.stdin); print('probe' if '$p' == '' else 'noprobe', d['value'], d['ms_per_step'])" || exit 1
   done
 done

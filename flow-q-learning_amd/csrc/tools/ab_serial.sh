@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box per-kernel A/B of builds on one stream (FQLPOP_SERIAL=1): a rocprofv3 kernel trace of
+# Same-box per-kernel A/B of builds on one stream (bench.py --serial): a rocprofv3 kernel trace of
 # a short bench per build, then each build's average for the kernels matching a regex.
 #   bash flow-q-learning_amd/csrc/tools/ab_serial.sh <regex> new ref ...   ("new" = the working
 #   tree's libfqlpop.so, X = fqlpop/libfqlpop_X.so through FQLPOP_LIB)
@@ -10,9 +10,9 @@ O=$R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 for f in "$@"; do
   if [ "$f" = new ]; then unset FQLPOP_LIB; else export FQLPOP_LIB=$R/flow-q-learning_amd/fqlpop/libfqlpop_$f.so; fi
-  export FQLPOP_SERIAL=1
+
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/abs_$f" -o run -- \
-      python3 "$R/bench.py" --steps 60 --warmup 10 --no-cpu-baseline --kernel-iters 1 --no-probe --preheat-ms 0 \
+      python3 "$R/bench.py" --diagnostic --serial --steps 60 --warmup 10 --no-cpu-baseline --kernel-iters 1 --no-probe --preheat-ms 0 \
       --eval-envs 0 --envmodel-train-steps 0 > "$O/abs_$f.log" 2>&1 || exit 1
   python3 - "$O/abs_$f/run_kernel_stats.csv" "$RX" "$f" <<'EOF'
 import csv, re, sys

@@ -1,9 +1,9 @@
 """Per-kernel MFMA utilisation and wave-state split of one serial-stream bench
 run from a rocprofv3 --pmc counter CSV (developer tool):
 
-  FQLPOP_SERIAL=1 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+  rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
       SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
-      -d out -o run -- python3 bench.py --steps 10 ...
+      -d out -o run -- python3 bench.py --serial --steps 10 ...
   python pmc_step_summary.py out/run_counter_collection.csv
 
 mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs): the

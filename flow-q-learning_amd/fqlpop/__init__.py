@@ -4,5 +4,6 @@
 (sibling packages) keep the reference's surface on top of it.
 """
 from fqlpop._lib import (EXPORTED_SYMBOLS, LIB_PATH, TRAIN_INFO_KEYS, VAL_INFO_KEYS,  # noqa: F401
-                         FqlpopError, load_library)
+                         FqlpopError, get_engine_option, is_diagnostic_build, load_library,
+                         reset_engine_options, set_engine_option)
 from fqlpop.population import Population, PopulationConfig  # noqa: F401

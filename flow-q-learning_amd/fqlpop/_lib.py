@@ -79,6 +79,10 @@ _F = ctypes.POINTER(ctypes.c_float)
 _U8 = ctypes.POINTER(ctypes.c_uint8)
 _SIGS = {
     "fqlpop_last_error": (ctypes.c_char_p, []),
+    "fqlpop_set_engine_option": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    "fqlpop_get_engine_option": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
+    "fqlpop_reset_engine_options": (ctypes.c_int, []),
+    "fqlpop_diagnostic_build": (ctypes.c_int, []),
     "fqlpop_create": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.c_int, _F,
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_int,
                                      ctypes.POINTER(_P)]),
@@ -164,6 +168,26 @@ def check(rc: int) -> None:
     if rc != 0:
         msg = load_library().fqlpop_last_error().decode(errors="replace")
         raise FqlpopError(f"fqlpop error {rc}: {msg}")
+
+
+def set_engine_option(name: str, value: int) -> None:
+    """Process-wide engine option for later Population handles (fqlpop_set_engine_option:
+    alternate code paths / stream schedules with the same results; tests and profiling)."""
+    check(load_library().fqlpop_set_engine_option(name.encode(), int(value)))
+
+
+def get_engine_option(name: str) -> int:
+    v = ctypes.c_int()
+    check(load_library().fqlpop_get_engine_option(name.encode(), ctypes.byref(v)))
+    return v.value
+
+
+def reset_engine_options() -> None:
+    check(load_library().fqlpop_reset_engine_options())
+
+
+def is_diagnostic_build() -> bool:
+    return bool(load_library().fqlpop_diagnostic_build())
 
 
 def fptr(a):

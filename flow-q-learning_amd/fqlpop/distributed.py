@@ -33,15 +33,17 @@ def broadcast_dataset(data: dict | None, shapes: dict, device: torch.device, src
     """Rank ``src`` holds ``data`` (numpy arrays); every rank returns torch tensors
     on ``device`` with the same contents (one broadcast per field)."""
     rank, ws = world()
+    # gloo (ranks sharing a device, CPU tests) moves host tensors; RCCL moves device tensors
+    stage = torch.device("cpu") if ws > 1 and dist.get_backend() == "gloo" else device
     out = {}
     for k in DATA_KEYS:
         if rank == src:
-            t = torch.from_numpy(np.ascontiguousarray(data[k], dtype=np.float32)).to(device)
+            t = torch.from_numpy(np.ascontiguousarray(data[k], dtype=np.float32)).to(stage)
         else:
-            t = torch.empty(shapes[k], dtype=torch.float32, device=device)
+            t = torch.empty(shapes[k], dtype=torch.float32, device=stage)
         if ws > 1:
             dist.broadcast(t, src=src)
-        out[k] = t
+        out[k] = t.to(device)
     return out
 
 
@@ -159,5 +161,16 @@ def gather_objects(obj, dst: int = 0):
 def eval_round_seed(base_seed: int, round_index: int) -> int:
     """Seed of the world-model evaluation of round ``round_index``: a function of
     the run seed and the round only, so a member's scores do not depend on the
-    sharding (the single-process Trainer draws it from the global np.random)."""
+    sharding or the world size (Trainer and DistributedTrainer alike)."""
     return int(np.random.default_rng([int(base_seed) & 0xFFFFFFFF, int(round_index)]).integers(0, 2**31 - 1))
+
+
+def member_eval_seed(base_seed: int, round_index: int, cfg) -> int:
+    """Seed of one candidate's own evaluation in round ``round_index`` (tasks without
+    a batched world-model evaluation): a function of the run seed, the round and the
+    candidate's (alpha, seed), so it does not depend on which rank owns the member."""
+    (fa, a), (fs, s) = config_key(cfg)
+    a_bits = int(np.array([a], dtype=np.float64).view(np.uint64)[0])
+    words = [int(base_seed) & 0xFFFFFFFF, int(round_index), fa, a_bits & 0xFFFFFFFF, a_bits >> 32, fs,
+             int(s) & 0xFFFFFFFF]
+    return int(np.random.default_rng(words).integers(0, 2**31 - 1))

@@ -19,9 +19,10 @@ the members it owns:
   step) from the most to the least loaded rank by point-to-point sends.  The
   device sampler is keyed by (seed, alpha, update count), not by slot or rank,
   so a moved member continues exactly as it would have in place;
-* the world-model evaluation seed of round r is ``eval_round_seed(config.seed,
-  r)``, so a member's scores -- and therefore every decision -- are the same for
-  every world size (the single-process Trainer draws it from np.random).
+* the evaluation of round r is seeded by ``eval_round_seed(config.seed, r)``
+  (world-model rollouts) or ``member_eval_seed(config.seed, r, config)``
+  (``Trainer._score``), so a member's scores -- and therefore every decision --
+  are the same for every world size and equal to the single-process Trainer's.
 
 ``state_dict()`` is collective: rank 0 returns the reference-shaped trainer
 state (every experiment ever created, candidates, RNG states), the other ranks
@@ -86,15 +87,6 @@ class DistributedTrainer(Trainer):
         self._free_slots.append(slot)
         return state
 
-    def _evaluate_round(self, configs) -> dict:
-        if not hasattr(self.task, "evaluate_members"):
-            return {}
-        members = [self.member_of[cfg] for cfg in configs if cfg in self.member_of]
-        if not members:
-            return {}
-        return self.task.evaluate_members(self.population, members,
-                                          D.eval_round_seed(self.config.seed, self.round_index))
-
     def _rebalance(self, live) -> None:
         for cfg, src, dst in D.rebalance_plan(live, self.owner, self.world_size):
             if self.rank == src:
@@ -139,7 +131,7 @@ class DistributedTrainer(Trainer):
                 done = exp.current_step == exp.steps
                 if done and cfg not in self.finished_candidates:
                     exp.save_agent()
-                results[cfg] = (exp.evaluate(round_eval.get(self.member_of.get(cfg))), done)
+                results[cfg] = (self._score(cfg, round_eval), done)
             merged = D.gather_scores(results)
             for cfg in this_round:  # the same order on every rank: identical strategy state
                 score, done = merged[cfg]

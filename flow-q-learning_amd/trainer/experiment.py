@@ -106,17 +106,18 @@ class Experiment:
                     self.log_step(info, val_info)
         return self.current_step == self.steps
 
-    def evaluate(self, eval_info: dict | None = None) -> float:
+    def evaluate(self, eval_info: dict | None = None, seed: int | None = None) -> float:
         """Success rate of the agent (reference :120-126).  Tasks with an on-GPU
         world model (``evaluate_members``) roll the member on the device;
-        ``eval_info`` passes a result the Trainer computed for a whole round."""
+        ``eval_info`` passes a result the Trainer computed for a whole round.
+        ``seed`` None draws the evaluation seed from np.random, as the reference does."""
         if eval_info is None:
             if hasattr(self.task, "evaluate_members") and self.agent.population is not None:
-                seed = int(np.random.randint(0, 2**31 - 1))
+                seed = int(np.random.randint(0, 2**31 - 1)) if seed is None else int(seed)
                 eval_info = self.task.evaluate_members(self.agent.population, [self.agent.member], seed)[
                     self.agent.member]
             else:
-                eval_info, _ = evaluate_agent(agent=self.agent, env=self.task)
+                eval_info, _ = evaluate_agent(agent=self.agent, env=self.task, seed=seed)
         self.logger.log(eval_info, step=self.current_step, group="eval")
         return eval_info.get("success", 0.0)
 

@@ -10,6 +10,13 @@ Deliberate fix: the strategy is updated with the
 candidate's ExperimentConfig, not the Experiment object (the reference passes
 ``self.experiments[config]`` at trainer/trainer.py:86, which breaks
 SuccessiveHalving because ``sample()`` then returns Experiments).
+
+Determinism across world sizes: candidates are visited in ``D.ordered`` order
+(the reference iterates a set), and the evaluation of round r is seeded by
+``D.eval_round_seed(seed, r)`` (world-model rollouts of the whole round) or
+``D.member_eval_seed(seed, r, config)`` (per-experiment evaluation), never by the
+global np.random stream.  So ``Trainer`` and ``DistributedTrainer`` at any world
+size score every member identically and take the same decisions.
 """
 from __future__ import annotations
 
@@ -19,6 +26,7 @@ import time
 import numpy as np
 
 from fqlpop import Population, PopulationConfig
+from fqlpop import distributed as D
 from hpo.strategy import HpoStrategy
 from task.task import Task
 from trainer.config import TrainerConfig
@@ -48,7 +56,9 @@ class Trainer:
             self.finished_candidates = state_dict["finished_candidates"]
             random.setstate(state_dict["random_rng_state"])
             np.random.set_state(state_dict["np_rng_state"])
+            self.round_index = int(state_dict.get("round_index", 0))
         else:
+            self.round_index = 0
             self.untrained_candidates = []
             self.finished_candidates = []
             self.candidates = sampled
@@ -100,6 +110,7 @@ class Trainer:
             "np_rng_state": np.random.get_state(),
             "untrained_candidates": self.untrained_candidates,
             "finished_candidates": self.finished_candidates,
+            "round_index": self.round_index,
         }
 
     # ---------------------------------------------------------------- train
@@ -125,11 +136,19 @@ class Trainer:
         members = [self.member_of[cfg] for cfg in configs if cfg in self.member_of]
         if not members:
             return {}
-        return self.task.evaluate_members(self.population, members, int(np.random.randint(0, 2**31 - 1)))
+        return self.task.evaluate_members(self.population, members,
+                                          D.eval_round_seed(self.config.seed, self.round_index))
+
+    def _score(self, cfg, round_eval: dict) -> float:
+        """The candidate's evaluation of this round: the round's world-model result, or
+        its own evaluation seeded by (run seed, round, candidate)."""
+        info = round_eval.get(self.member_of.get(cfg))
+        seed = None if info is not None else D.member_eval_seed(self.config.seed, self.round_index, cfg)
+        return self.experiments[cfg].evaluate(info, seed=seed)
 
     def train(self, max_evaluations: int) -> None:
         while max_evaluations > 0:
-            queue = list(self.untrained_candidates) if self.untrained_candidates else list(self.candidates)
+            queue = list(self.untrained_candidates) if self.untrained_candidates else D.ordered(self.candidates)
             this_round, deferred = queue[:max_evaluations], queue[max_evaluations:]
             start = time.perf_counter()
             self._train_round(this_round)
@@ -139,9 +158,9 @@ class Trainer:
                 if exp.current_step == exp.steps and cfg not in self.finished_candidates:
                     exp.save_agent()
                     self.finished_candidates.append(cfg)
-                score = exp.evaluate(round_eval.get(self.member_of.get(cfg)))
-                self.strategy.update(cfg, score)
+                self.strategy.update(cfg, self._score(cfg, round_eval))
                 max_evaluations -= 1
+            self.round_index += 1
             print(f"Elapsed time: {time.perf_counter() - start:.6f} seconds ({len(this_round)} candidates)")
             if deferred:
                 self.untrained_candidates = deferred

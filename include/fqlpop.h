@@ -73,6 +73,21 @@ typedef struct fqlpop fqlpop_t;
 /* Message of the last failed call on this thread ("" if none). */
 const char* fqlpop_last_error(void);
 
+/* Engine options: process-wide defaults read by every later fqlpop_create.  They
+ * select alternate code paths and stream schedules with the same results
+ * (bit-identical, or the per-layer / unfused paths within the parity tolerance),
+ * for tests and profiling; there is no reference counterpart.  Names:
+ *   euler_fused, stream_fwd, stream_bwd, fused_adam, cdw_sb, serial  (0/1)
+ *   streams (3/4), prio (0..2), dw_tile_critic / dw_tile_actor (0..10), adam_nt (0..3).
+ * The defaults are the measured-fastest configuration.  Unknown names or values
+ * out of range: FQLPOP_E_ARG.  The production library reads no environment
+ * variable; result-changing timing switches exist only in diagnostic builds. */
+int fqlpop_set_engine_option(const char* name, int value);
+int fqlpop_get_engine_option(const char* name, int* value);
+int fqlpop_reset_engine_options(void);
+/* 1 in a diagnostic build (make DIAG=1 / PHASE=1), 0 in the production library. */
+int fqlpop_diagnostic_build(void);
+
 /* Replaces FQLAgent.create(seed, ex_obs, ex_act, config)  [EXT]
  * (called at trainer/experiment.py:44-49, utils/agent.py:24-29) for a whole
  * population: allocates the device state for n_members members, member i

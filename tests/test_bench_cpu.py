@@ -1,0 +1,52 @@
+"""bench.py's refusals, which happen before any GPU call (CPU tests), and the
+production library's switch hygiene."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env):
+    e = {k: v for k, v in os.environ.items() if not k.startswith("FQLPOP_")}
+    e.update(env)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True,
+                          text=True, timeout=120, cwd=ROOT, env=e)
+
+
+def test_bench_refuses_developer_switches():
+    r = _bench(["--steps", "1"], {"FQLPOP_SKIP": "1"})
+    assert r.returncode == 2 and "FQLPOP_SKIP" in r.stderr
+
+
+def test_bench_refuses_world_size_mismatch():
+    r = _bench(["--gpus", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "!= --gpus" in r.stderr
+
+
+def test_production_library_reads_no_environment():
+    """The shipped libfqlpop.so is not a diagnostic build and imports no getenv: the
+    timing-only switches (FQLPOP_SKIP, FQLPOP_DW_MODE, FQLPOP_PIPE_EXP, FQLPOP_PHASE_PROBE)
+    cannot reach it.  Alternate code paths go through fqlpop_set_engine_option."""
+    import fqlpop
+    assert not fqlpop.is_diagnostic_build()
+    out = subprocess.run(["nm", "-D", "--undefined-only", fqlpop.LIB_PATH], capture_output=True, text=True)
+    assert out.returncode == 0
+    assert "getenv" not in out.stdout
+    with open(fqlpop.LIB_PATH, "rb") as f:
+        blob = f.read()
+    for name in (b"FQLPOP_SKIP", b"FQLPOP_DW_MODE", b"FQLPOP_PIPE_EXP", b"FQLPOP_PHASE_PROBE"):
+        assert name not in blob, name
+
+
+def test_engine_options_validate_and_reset():
+    import pytest
+    import fqlpop
+    fqlpop.set_engine_option("serial", 1)
+    assert fqlpop.get_engine_option("serial") == 1
+    fqlpop.reset_engine_options()
+    assert fqlpop.get_engine_option("serial") == 0
+    with pytest.raises(fqlpop.FqlpopError):
+        fqlpop.set_engine_option("no_such_option", 1)
+    with pytest.raises(fqlpop.FqlpopError):
+        fqlpop.set_engine_option("streams", 7)

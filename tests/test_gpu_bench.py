@@ -33,3 +33,42 @@ def test_bench_json_contract():
     assert rf["launches_timed"] == 4  # one probed dominant launch per timed step
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert d["preheat"]["ms"] > 0
+
+
+def _bench(args, env=None, timeout=400):
+    e = dict(os.environ)
+    for k in [k for k in e if k.startswith("FQLPOP_")]:
+        del e[k]
+    e.update(env or {})
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), *args]
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=e)
+
+
+def test_bench_self_launches_ranks_sharing_the_device():
+    """bench.py --gpus 2 without torch.distributed.run starts its own two rank processes
+    (the parent makes no GPU call); --share-device puts both on cuda:0 over gloo.  The
+    JSON line counts both ranks' members and is printed once."""
+    r = _bench(["--gpus", "2", "--share-device", "--steps", "4", "--warmup", "2", "--rows", "20000",
+                "--no-cpu-baseline", "--eval-envs", "0", "--envmodel-train-steps", "0", "--kernel-iters", "2",
+                "--preheat-ms", "20", "--members", "4"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["share_device"] is True
+    assert d["config"]["global_batch"] == 256 * 4 * 2
+    assert abs(d["value"] - 8 * 1000.0 / d["ms_per_step"]) <= 1e-3 * d["value"] + 1.0
+    assert d["config"]["info_finite"] is True
+    assert "gpu_clock" in d and "start" in d["gpu_clock"]
+
+
+def test_production_library_ignores_timing_switches():
+    """FQLPOP_SKIP (leave launches out) and FQLPOP_DW_MODE (drop optimiser phases) only
+    exist in diagnostic builds: with them set, the production library's update still
+    matches the oracle."""
+    code = ("import sys; sys.path[:0] = [%r, %r]; import __graft_entry__ as g; g.smoke()"
+            % (ROOT, os.path.join(ROOT, "flow-q-learning_amd")))
+    e = dict(os.environ, FQLPOP_SKIP="255", FQLPOP_DW_MODE="1", FQLPOP_PIPE_EXP="1", FQLPOP_PHASE_PROBE="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=ROOT, env=e)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "smoke ok" in r.stdout

@@ -20,7 +20,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(rank, world, port, save_dir, strategy_kind):
+def _run(rank, world, port, save_dir, strategy_kind, plain=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (root, os.path.join(root, "flow-q-learning_amd")):
@@ -36,6 +36,7 @@ def _run(rank, world, port, save_dir, strategy_kind):
     from task.offline_task_simulated import OfflineTaskWithSimulatedEvaluations
     from trainer.config import AgentConfig, ExperimentConfig, TrainerConfig
     from trainer.distributed_trainer import DistributedTrainer
+    from trainer.trainer import Trainer
 
     class KeepEven(HpoStrategy):
         """After two evaluations keep the candidates at even positions of the
@@ -62,7 +63,7 @@ def _run(rank, world, port, save_dir, strategy_kind):
         strategy = SuccessiveHalving(configs, total_evaluations=12, fraction=0.5, history_length=1)
     else:
         strategy = KeepEven(configs)
-    tr = DistributedTrainer(task, strategy, cfg)
+    tr = Trainer(task, strategy, cfg) if plain else DistributedTrainer(task, strategy, cfg)
     tr.train(max_evaluations=100)
     state = tr.state_dict()
     params = {str(c): np.concatenate([v.ravel() for net in e.agent.to_state_dict()["params"].values()
@@ -71,7 +72,7 @@ def _run(rank, world, port, save_dir, strategy_kind):
     scores = {str(c): list(v) for c, v in getattr(strategy, "candidate_scores", {}).items()}
     out = dict(rank=rank, candidates=sorted(str(c) for c in tr.candidates), params=params, steps=steps,
                scores=scores, n_state=None if state is None else len(state["experiments"]),
-               owners={str(c): r for c, r in tr.owner.items() if c in tr.candidates})
+               owners={str(c): r for c, r in getattr(tr, "owner", {}).items() if c in tr.candidates})
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -104,7 +105,13 @@ def _two_ranks(tmp_path, kind):
 
 @pytest.mark.parametrize("kind", ["halving", "keep_even"])
 def test_two_ranks_match_one_rank(tmp_path, kind):
-    one = _run(0, 1, 0, str(tmp_path / "w1"), kind)
+    """The baseline is the plain single-process Trainer (what tune_alpha runs at
+    WORLD_SIZE=1); DistributedTrainer at one rank must agree with it too."""
+    one = _run(0, 1, 0, str(tmp_path / "w1"), kind, plain=True)
+    one_d = _run(0, 1, 0, str(tmp_path / "w1d"), kind)
+    assert one_d["candidates"] == one["candidates"] and one_d["scores"] == one["scores"]
+    for c, p in one_d["params"].items():
+        np.testing.assert_array_equal(p, one["params"][c])
     r0, r1 = _two_ranks(tmp_path, kind)
     # the same decisions and scores on every rank, equal to the one-rank run
     assert r0["candidates"] == r1["candidates"] == one["candidates"]
