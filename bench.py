@@ -313,6 +313,9 @@ def main(argv=None):
                     help="every rank on cuda:0 over gloo (rehearse the N-rank path on one GPU)")
     ap.add_argument("--serial", action="store_true",
                     help="profiling: every launch of the step on one stream (engine option serial)")
+    ap.add_argument("--engine-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="fqlpop_set_engine_option before the population is created (alternate schedules / "
+                         "code paths with the same results; recorded in the JSON line)")
     ap.add_argument("--diagnostic", action="store_true",
                     help="allow FQLPOP_* environment variables (developer A/B runs); they are recorded")
     args = ap.parse_args(argv)
@@ -347,8 +350,14 @@ def main(argv=None):
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
 
     from fqlpop import Population, PopulationConfig, set_engine_option
+    engine_opts = {}
+    for kv in args.engine_option:
+        k, v = kv.split("=", 1)
+        engine_opts[k] = int(v)
     if args.serial:
-        set_engine_option("serial", 1)
+        engine_opts["serial"] = 1
+    for k, v in engine_opts.items():
+        set_engine_option(k, v)
 
     wl = WORKLOADS[args.workload]
     # dataset: generated on rank 0, broadcast over RCCL (xGMI) to every rank
@@ -463,6 +472,7 @@ def main(argv=None):
             "info_finite": finite,
             "share_device": bool(args.share_device),
             "serial_streams": bool(args.serial),
+            "engine_options": engine_opts,
         },
         "gpu_clock": {"device": torch.cuda.get_device_name(dev_index), "start": clk0, "end": clk1,
                       "note": "sysfs pp_dpm_sclk / hwmon of this rank's GPU, read just before the clock "

@@ -90,6 +90,7 @@ struct AdamEpi {
     int mode;                         // 0; timing probes (FQLPOP_DW_MODE): 1 = no optimiser pass, 2 = one k-slice,
                                       // 3 = no W^T pass
     int nt;                           // non-temporal optimiser streams: 1 m/v, 2 target, 4 p_in, 8 p_out/W^T
+    int stagger;                      // first-wave start offsets (s_sleep 32 units per co-resident rank), 0 = off
     // the net's small leaves (biases, LN, head) ride in the same launch: blocks past the
     // GEMM tiles run the adam_kernel body on small.ids chunks (small_blocks = chunks x nz)
     AdamArgs small;

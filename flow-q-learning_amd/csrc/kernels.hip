@@ -667,6 +667,16 @@ DEV void gemm_group_body(const GemmGroupArgs& ga, float* smem) {
         adam_chunk(ga.adam.small, sb % nch, sb / nch);
         return;
     }
+    if constexpr (EPI == EPI_ADAM) {
+        // staggered start of the first dispatch wave (blocks b, b + 256, b + 512, b + 768 share
+        // a CU): co-resident blocks then reach their HBM-bound optimiser pass at different
+        // times instead of all running the k-loop, then all streaming, in lock step
+        const int st = ga.adam.stagger;
+        if (st > 0 && (int)blockIdx.x < 1024) {
+            const int n = (((int)blockIdx.x >> 8) & 3) * st;
+            for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(32);
+        }
+    }
     const int bid = xcd_remap(blockIdx.x, ga.first[ga.ng]);
     int gi = 0;
 #pragma unroll

@@ -77,6 +77,7 @@ struct EngineOptions {
     int prio = 0;          // stream priorities: 1 main chain high, 2 flow high
     int dw_tile_critic = 10, dw_tile_actor = 10;  // grouped dW tile ids (launch_gemm_group_dw)
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
+    int dw_stagger = 0;    // fused dW + optimiser: first-wave start offsets (AdamEpi::stagger)
 };
 EngineOptions g_engine_opts;
 
@@ -93,6 +94,7 @@ const EngineOptionRef kEngineOptions[] = {
     {"dw_tile_critic", &EngineOptions::dw_tile_critic, 0, 10},
     {"dw_tile_actor", &EngineOptions::dw_tile_actor, 0, 10},
     {"adam_nt", &EngineOptions::adam_nt, 0, 3},
+    {"dw_stagger", &EngineOptions::dw_stagger, 0, 256},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -767,6 +769,7 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
             // need not displace the weights the streamed kernels re-read from L2 / MALL
             // (+1.0 % same-box; engine option adam_nt: bit mask, see AdamEpi::nt)
             ae.nt = h->opt.adam_nt;
+            ae.stagger = h->opt.dw_stagger;
         }
         ae.small = adam_args(c, ni);
         ae.small_blocks = ae.small.n_chunks * c.nz;

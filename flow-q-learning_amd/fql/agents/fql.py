@@ -24,8 +24,20 @@ from __future__ import annotations
 
 import numpy as np
 
+from fql.utils.serialization import flat_to_flax, flax_to_flat, is_flax_layout
 from fqlpop import Population, PopulationConfig
 from fqlpop._lib import TRAIN_INFO_KEYS, VAL_INFO_KEYS
+
+
+def _sampler_key(seed: int, alpha: float) -> int:
+    """The device sampler's member key (runtime.cpp sample_key: splitmix64 finaliser of
+    seed ^ (bits(float32 alpha) << 32 | 0x9E3779B9))."""
+    m = (1 << 64) - 1
+    ab = int(np.array([alpha], dtype=np.float32).view(np.uint32)[0])
+    z = (int(seed) ^ ((ab << 32) | 0x9E3779B9)) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
 
 
 def _as_seed(seed) -> int:
@@ -89,10 +101,17 @@ class FQLAgent:
 
     # ----------------------------------------------------------- state dict
     def to_state_dict(self) -> dict:
-        return self.population.state_dict(self.member)
+        """``flax.serialization.to_state_dict(agent)`` layout (fql/utils/serialization.py):
+        {rng, network: {step, params: {modules_<net>: ...}, opt_state}}.  ``rng`` holds the
+        member's device sampler key (Philox, keyed by seed and alpha) as two uint32 words."""
+        pop = self.population
+        key = _sampler_key(int(pop.seeds[self.member]), float(pop.alphas[self.member]))
+        return flat_to_flax(pop.state_dict(self.member), rng=[key & 0xFFFFFFFF, key >> 32])
 
     def from_state_dict(self, sd: dict):
-        self.population.load_state_dict(self.member, sd)
+        """Accepts the flax layout or the engine's flat member state (older checkpoints)."""
+        flat = flax_to_flat(sd) if is_flax_layout(sd) else sd
+        self.population.load_state_dict(self.member, flat)
         return self
 
     @property

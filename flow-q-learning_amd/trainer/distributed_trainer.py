@@ -76,6 +76,11 @@ class DistributedTrainer(Trainer):
             self.create_experiment(cfg, state_dict=saved.get(cfg))
         if self.rank == 0:  # experiments that are no longer candidates: re-emitted by rank 0's state_dict
             self.retired = {c: s for c, s in saved.items() if c not in self.owner}
+        # holder[c]: the rank that keeps the state of a stopped experiment c (the same map on
+        # every rank), so that a strategy that brings c back (SuccessiveHalving ranks every
+        # candidate it has scores for, hpo/successive_halving.py:83-97) resumes it, not a
+        # fresh one
+        self.holder = {c: 0 for c in saved if c not in self.owner}
 
     # ------------------------------------------------------------ members
     def _release(self, cfg) -> dict:
@@ -151,14 +156,26 @@ class DistributedTrainer(Trainer):
                 break
             new_candidates = self.strategy.sample()
             for cfg in D.ordered(self.candidates):
-                if cfg not in new_candidates and self.owner.get(cfg) == self.rank:
-                    self.retired[cfg] = self._release(cfg)
+                if cfg not in new_candidates:
+                    src = self.owner.pop(cfg)
+                    self.holder[cfg] = src
+                    if src == self.rank:
+                        self.retired[cfg] = self._release(cfg)
             live = D.ordered(new_candidates)
             for cfg, r in D.place_new([c for c in live if c not in self.owner], live, self.owner,
                                       self.world_size).items():
                 self.owner[cfg] = r
-                if r == self.rank:
-                    self.create_experiment(cfg)
+                src = self.holder.pop(cfg, None)
+                if src is None:  # a new candidate
+                    if r == self.rank:
+                        self.create_experiment(cfg)
+                elif src == r:   # a stopped candidate brought back on the rank that holds it
+                    if r == self.rank:
+                        self.create_experiment(cfg, state_dict=self.retired.pop(cfg))
+                elif self.rank == src:
+                    D.send_object(self.retired.pop(cfg), r)
+                elif self.rank == r:
+                    self.create_experiment(cfg, state_dict=D.recv_object(src))
             self._rebalance(live)
             self.candidates = new_candidates
         for exp in self.experiments.values():

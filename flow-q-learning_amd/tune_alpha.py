@@ -66,6 +66,13 @@ def main(argv=None):
     parser.add_argument("--strategy", choices=("identity", "successive_halving"), default="identity")
     parser.add_argument("--fraction", type=float, default=0.5)
     parser.add_argument("--history_length", type=int, default=1)
+    # SuccessiveHalving's evaluation horizon E (hpo/successive_halving.py milestones).  The
+    # reference passes --max_evaluations, which Trainer.train spends per candidate: with N
+    # candidates evaluated every round the milestones (in evaluations per candidate, >= h)
+    # are then out of reach for N >= 8 at h = 4.  The reference's StrategyEvaluator counts E in
+    # rounds (steps / eval_interval); --halving_horizon selects that reading.  Default: the
+    # reference wiring.
+    parser.add_argument("--halving_horizon", type=int, default=None)
     args = parser.parse_args(argv)
     config = build_config_from_args(args)
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,7 +116,8 @@ def main(argv=None):
     if args.strategy == "identity":
         strategy = Identity(population=configs, total_evaluations=0, state_dict=state.get("strategy"))
     else:
-        strategy = SuccessiveHalving(population=set(configs), total_evaluations=args.max_evaluations,
+        horizon = args.max_evaluations if args.halving_horizon is None else args.halving_horizon
+        strategy = SuccessiveHalving(population=set(configs), total_evaluations=horizon,
                                      fraction=args.fraction, history_length=args.history_length,
                                      state_dict=state.get("strategy"))
     if world_size > 1:

@@ -16,6 +16,7 @@ except Exception:  # pragma: no cover
 
 class CsvLogger:
     def __init__(self, path, resume: bool = False):
+        self.path = path
         os.makedirs(os.path.dirname(path), exist_ok=True)
         self.header = None
         if resume and os.path.exists(path) and os.path.getsize(path) > 0:
@@ -27,6 +28,8 @@ class CsvLogger:
         row = dict(row)
         if step is not None:
             row["step"] = step
+        if self.file is None:  # a stopped experiment that a strategy brought back appends
+            self.file = open(self.path, "a")
         if self.header is None:
             self.header = list(row)
             self.file.write(",".join(self.header) + "\n")

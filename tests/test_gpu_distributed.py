@@ -66,9 +66,11 @@ def _run(rank, world, port, save_dir, strategy_kind, plain=False):
     tr = Trainer(task, strategy, cfg) if plain else DistributedTrainer(task, strategy, cfg)
     tr.train(max_evaluations=100)
     state = tr.state_dict()
-    params = {str(c): np.concatenate([v.ravel() for net in e.agent.to_state_dict()["params"].values()
-                                      for v in net.values()]) for c, e in tr.experiments.items()}
-    steps = {str(c): e.current_step for c, e in tr.experiments.items()}
+    from fql.utils.serialization import params_of
+    live = {c: e for c, e in tr.experiments.items() if c in tr.candidates}  # Trainer keeps stopped ones too
+    params = {str(c): np.concatenate([v.ravel() for net in params_of(e.agent.to_state_dict()).values()
+                                      for v in net.values()]) for c, e in live.items()}
+    steps = {str(c): e.current_step for c, e in live.items()}
     scores = {str(c): list(v) for c, v in getattr(strategy, "candidate_scores", {}).items()}
     out = dict(rank=rank, candidates=sorted(str(c) for c in tr.candidates), params=params, steps=steps,
                scores=scores, n_state=None if state is None else len(state["experiments"]),

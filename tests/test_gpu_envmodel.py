@@ -153,3 +153,25 @@ def test_simulated_task_trainer_halving(tmp_path):
     task.attach(tr.population)
     info, transitions = evaluate_agent(exp.agent, task, seed=0)
     assert 0.0 <= info["success"] <= 1.0 and len(transitions) <= 25
+
+
+def test_rollout_antsoccer_32_members_matches_oracle():
+    """BASELINE config C5's evaluation at its shapes: 32 members of the antsoccer actor
+    (obs 42, act 8, 512 x 4) x 50 envs (eval_episodes) in one launch, with the
+    multistep default state predictor (128, 256, 128) and a termination predictor that
+    ends some episodes.  Success flags and episode lengths must equal the oracle's for
+    every env of every member; observations of the envs still running after the last
+    step within 2e-3."""
+    n = 32
+    pop, cfg, params = _population(n, 42, 8, seed=40)
+    spec = em.EnvModelSpec(42, 8, (128, 256, 128), (128, 128))
+    sp, tp = _env_model(spec, tp_bias=4.0, tp_scale=3.0, seed=21)  # ~12 % terminate; |logit| > 0.7 throughout
+    _upload(pop, spec, sp, tp)
+    succ, length, oobs, want = _run_both(pop, cfg, params, spec, sp, tp, n_envs=50, steps=8, seed=9)
+    assert succ.shape == (n, 50)
+    for i, (s, l, obs, _) in enumerate(want):
+        np.testing.assert_array_equal(succ[i], s, err_msg=f"member {i}")
+        np.testing.assert_array_equal(length[i], l, err_msg=f"member {i}")
+        np.testing.assert_allclose(oobs[i], obs, rtol=2e-3, atol=2e-4, err_msg=f"member {i}")
+    assert 0 < succ.mean() < 1, succ.mean()  # both outcomes occur
+    pop.close()

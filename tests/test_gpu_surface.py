@@ -49,11 +49,17 @@ def test_fqlagent_surface():
     batch = O.cast_tree(O.make_batch(ocfg, 64, rng), np.float32)
     agent = FQLAgent.create(3, batch["observations"][:1], batch["actions"][:1], cfg)
     assert agent.config["ob_dims"] == (28,) and agent.config["action_dim"] == 5
-    before = agent.to_state_dict()["params"]["actor_onestep_flow"]["Dense_0/kernel"].copy()
+    sd0 = agent.to_state_dict()
+    assert set(sd0) == {"rng", "network"} and set(sd0["network"]) == {"step", "params", "opt_state"}
+    assert set(sd0["network"]["params"]) == {"modules_actor_bc_flow", "modules_actor_onestep_flow",
+                                             "modules_critic", "modules_target_critic"}
+    before = sd0["network"]["params"]["modules_actor_onestep_flow"]["mlp"]["Dense_0"]["kernel"].copy()
     agent, info = agent.update(batch)
     assert set(info) == set(O.TRAIN_INFO_KEYS) and all(np.isfinite(v) for v in info.values())
     assert agent.step == 1
-    after = agent.to_state_dict()["params"]["actor_onestep_flow"]["Dense_0/kernel"]
+    sd1 = agent.to_state_dict()
+    after = sd1["network"]["params"]["modules_actor_onestep_flow"]["mlp"]["Dense_0"]["kernel"]
+    assert sd1["network"]["step"] == 1 and int(sd1["network"]["opt_state"]["0"]["count"]) == 1
     assert not np.array_equal(before, after)
     loss, vinfo = agent.total_loss(batch, grad_params=None)
     assert set(vinfo) == set(O.VAL_INFO_KEYS) and np.isfinite(loss)
@@ -119,8 +125,9 @@ def test_population_members_are_independent_in_trainer(tmp_path):
     t_pair.train(max_evaluations=2)
     t_solo = Trainer(task, Identity([c2], 0), cfg)
     t_solo.train(max_evaluations=1)
-    a = t_pair.experiments[c2].agent.to_state_dict()["params"]
-    b = t_solo.experiments[c2].agent.to_state_dict()["params"]
+    from fql.utils.serialization import params_of
+    a = params_of(t_pair.experiments[c2].agent.to_state_dict())
+    b = params_of(t_solo.experiments[c2].agent.to_state_dict())
     for net in O.NETS:
         for leaf in a[net]:
             assert np.array_equal(a[net][leaf], b[net][leaf]), (net, leaf)
