@@ -698,6 +698,418 @@ __global__ __launch_bounds__(256, 4) void gemm_group_kernel_o4(const GemmGroupAr
     gemm_group_body<BM, BN, ARC, BRC, EPI, BK>(ga, smem);
 }
 
+// ---------------------------------------------- wave-specialised dW + optimiser ----
+// The same work as gemm_group_kernel_o4<64, 128, true, true, EPI_ADAM, 16> (tile id 14),
+// bit-identical, in a persistent launch whose blocks split their 8 waves into two groups
+// that run concurrently:
+//   G (waves 0-3): the dW k-loop of tile n (the same MFMA sequence as gemm_body, KB layout);
+//   O (waves 4-7): optax.adam / the target EMA / grad stats / the W^T copy of tile n-1, from
+//                  the gradient tile G left in LDS, with its p / m / v / target loads issued
+//                  two units ahead across the phase barriers.
+// A tile period is NPH = max(k-slices, 16) phases, each ending in one raw s_barrier that both
+// groups execute (no vmcnt(0): O's loads stay in flight across it); at the period boundary G
+// writes its accumulators into the gradient tile and one more barrier publishes it.  In the
+// one-tile-per-block launch every co-resident block ran its k-loop, then its HBM-bound
+// optimiser pass, at the same time as the others (they start together), so the two phases
+// hardly overlapped; here each CU has both kinds of work in flight all the time.
+constexpr int WS_BM = 64, WS_BN = 128, WS_BK = 16, WS_RP = 20, WS_PT = WS_BN + 1, WS_NU = 8;
+constexpr int WS_SMEM = 2 * (WS_BM + WS_BN) * WS_RP + WS_BM * WS_PT + 16;
+
+DEV void ws_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// block-uniform description of logical tile lt of a grouped launch
+struct WsTile {
+    int gi, slot, y, tile, per, i0, j0;
+};
+DEV WsTile ws_tile(const GemmGroupArgs& ga, int lt) {
+    int gi = 0;
+#pragma unroll
+    for (int i = 1; i < GEMM_GROUP_MAX; ++i)
+        if (i < ga.ng && lt >= ga.first[i]) gi = i;
+    gi = uni(gi);
+    const GemmArgs& g = ga.g[gi];
+    const int gM = uni(g.M), gN = uni(g.N), gny = uni(g.ny);
+    const int tiles_m = gM / WS_BM + (gM % WS_BM != 0), tiles_n = gN / WS_BN;
+    const int per = tiles_m * tiles_n, w = lt - uni(ga.first[gi]);
+    const int tile = w % per, yz = w / per;
+    WsTile t;
+    t.gi = gi; t.per = per; t.tile = tile;
+    t.y = yz % gny;
+    t.slot = uni(g.slots[yz / gny]);
+    t.i0 = (tile / tiles_n) * WS_BM;
+    t.j0 = (tile % tiles_n) * WS_BN;
+    return t;
+}
+
+// block-level sums over 8 waves where waves 4-7 contribute the identity: the same value (and
+// bits) as block_sum over waves 0-3
+DEV float ws_block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+DEV float ws_block_max(float v, float* red) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+DEV float ws_block_min(float v, float* red) {
+    v = wave_min(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
+}
+
+// adam_chunk for a 512-thread block: threads 0..255 do exactly adam_chunk's work (same
+// per-thread order, same reduction order), threads 256..511 only join the barriers
+DEV void adam_chunk_ws(const AdamArgs& a, int bx, int z) {
+    const int ci = a.ids ? a.ids[bx] : a.chunk_base + bx;
+    const int slot = a.slots[z];
+    const Chunk ck = a.chunks[ci];
+    const long long base = (long long)slot * a.P + a.net_off + ck.off;
+    const float t = (float)(a.count[slot] + 1);
+    const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
+    float mx = -INFINITY, mn = INFINITY, ss = 0.f;
+    const float lr = a.lr, tau = a.tau;
+    const bool hasT = a.target != nullptr;
+    if (threadIdx.x < 256) {
+        const float* __restrict__ Pin = a.p_in + base;
+        float* __restrict__ P = a.p_out + base;
+        const float* __restrict__ G = a.g + base;
+        float* __restrict__ Mm = a.m + base;
+        float* __restrict__ V = a.v + base;
+        float* __restrict__ T = hasT ? a.target + (long long)slot * a.PT + ck.off : nullptr;
+#define FQ_ADAM1(g, p, m, v, hasT, tp)                              \
+    do {                                                            \
+        m = 0.1f * (g) + 0.9f * m;                                  \
+        v = 0.001f * ((g) * (g)) + 0.999f * v;                      \
+        const float mh_ = m / bc1, vh_ = v / bc2;                   \
+        if (hasT) tp = tau * p + (1.0f - tau) * tp;                 \
+        p = p + (-lr) * (mh_ / (sqrtf(vh_) + 1e-8f));               \
+        mx = fmaxf(mx, (g));                                        \
+        mn = fminf(mn, (g));                                        \
+        ss += (g) * (g);                                            \
+    } while (0)
+        if ((ck.len & 3) == 0) {
+            for (int i = threadIdx.x * 4; i < ck.len; i += 1024) {
+                const float4 g4 = *reinterpret_cast<const float4*>(G + i);
+                float4 p4 = *reinterpret_cast<const float4*>(Pin + i);
+                float4 m4 = *reinterpret_cast<float4*>(Mm + i);
+                float4 v4 = *reinterpret_cast<float4*>(V + i);
+                float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (hasT) t4 = *reinterpret_cast<float4*>(T + i);
+                FQ_ADAM1(g4.x, p4.x, m4.x, v4.x, hasT, t4.x);
+                FQ_ADAM1(g4.y, p4.y, m4.y, v4.y, hasT, t4.y);
+                FQ_ADAM1(g4.z, p4.z, m4.z, v4.z, hasT, t4.z);
+                FQ_ADAM1(g4.w, p4.w, m4.w, v4.w, hasT, t4.w);
+                *reinterpret_cast<float4*>(P + i) = p4;
+                *reinterpret_cast<float4*>(Mm + i) = m4;
+                *reinterpret_cast<float4*>(V + i) = v4;
+                if (hasT) *reinterpret_cast<float4*>(T + i) = t4;
+            }
+        } else {
+            for (int i = threadIdx.x; i < ck.len; i += 256) {
+                const float gv = G[i];
+                float p = Pin[i], m = Mm[i], v = V[i], tv = hasT ? T[i] : 0.f;
+                FQ_ADAM1(gv, p, m, v, hasT, tv);
+                P[i] = p;
+                Mm[i] = m;
+                V[i] = v;
+                if (hasT) T[i] = tv;
+            }
+        }
+#undef FQ_ADAM1
+    }
+    __shared__ float red[8];
+    mx = ws_block_max(mx, red);
+    mn = ws_block_min(mn, red);
+    ss = ws_block_sum(ss, red);
+    if (threadIdx.x == 0) {
+        float* st = a.stats + ((long long)slot * a.n_total_chunks + ci) * 3;
+        st[0] = mx;
+        st[1] = mn;
+        st[2] = ss;
+    }
+}
+
+__global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga) {
+    __shared__ __attribute__((aligned(16))) float smem[WS_SMEM];
+    constexpr int BM = WS_BM, BN = WS_BN, BK = WS_BK, RP = WS_RP, PT = WS_PT;
+    const int nper = ga.adam.persist;  // persistent blocks (a multiple of 8)
+    if ((int)blockIdx.x >= nper) {
+        const int sb = blockIdx.x - nper, nch = ga.adam.small.n_chunks;
+        adam_chunk_ws(ga.adam.small, sb % nch, sb / nch);
+        return;
+    }
+    const int T = ga.first[ga.ng];
+    // the XCD's contiguous range of logical tiles (as xcd_remap), dealt round-robin to its blocks
+    const int q8 = T >> 3, r8 = T & 7, x = blockIdx.x & 7, jb = blockIdx.x >> 3, nbx = nper >> 3;
+    const int start = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+    const int cnt = q8 + (x < r8 ? 1 : 0);
+    const int ntl = jb < cnt ? (cnt - jb + nbx - 1) / nbx : 0;
+    if (ntl == 0) return;
+    auto tile_id = [&](int n) { return start + jb + n * nbx; };
+    const int gK = uni(ga.g[0].K);  // one net: every problem has K = Mg
+    const int nk = (gK + BK - 1) / BK;
+    const int nph = nk > 2 * WS_NU ? nk : 2 * WS_NU;
+    float* const As0 = smem;
+    float* const Bs0 = smem + BM * RP;
+    float* const As1 = smem + (BM + BN) * RP;
+    float* const Bs1 = As1 + BM * RP;
+    float* const Gt = smem + 2 * (BM + BN) * RP;  // gradient tile [BM][PT], then the new p
+    float* const red = Gt + BM * PT;             // [12]: O-wave stats partials
+    const AdamEpi& e = ga.adam;
+    const int wave = threadIdx.x >> 6;
+
+    if (wave < 4) {
+        // ------------------------------------------------------------ G: the k-loops
+        const int tid = threadIdx.x, lane = tid & 63;
+        const int wi = (wave >> 1) * (BM / 2), wj = (wave & 1) * (BN / 2);
+        const int l32 = lane & 31, lh = lane >> 5;
+        constexpr int A_LD = BM * BK / 1024, B_LD = BN * BK / 1024;
+        float4 ra[A_LD], rb[B_LD];
+        f32x16 acc[2];
+        WsTile t = ws_tile(ga, tile_id(0));
+        auto rsrcs = [&](const WsTile& tt, rsrc_t& rA, rsrc_t& rB, int& lda, int& ldb) {
+            const GemmArgs& g = ga.g[tt.gi];
+            const int gM = uni(g.M), gN = uni(g.N);
+            lda = uni(g.lda);
+            ldb = uni(g.ldb);
+            rA = make_rsrc(uniptr(at(g.A, tt.slot, tt.y)), (long long)(gM - 1) * lda + gK);
+            rB = make_rsrc(uniptr(at(g.B, tt.slot, tt.y)), (long long)(gN - 1) * ldb + gK);
+        };
+        rsrc_t rA, rB;
+        int lda, ldb;
+        rsrcs(t, rA, rB, lda, ldb);
+        // prologue: slice 0 of the first tile
+#pragma unroll
+        for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, true>(rA, lda, p, t.i0, 0);
+#pragma unroll
+        for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, true>(rB, ldb, p, t.j0, 0);
+#pragma unroll
+        for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, true, RP>(As0, p, ra[p]);
+#pragma unroll
+        for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, true, RP>(Bs0, p, rb[p]);
+        ws_barrier();
+        for (int it = 0; it <= ntl; ++it) {
+            const bool work = it < ntl;
+            // the slices' source: this tile, then in the last phase the next tile's slice 0
+            WsTile tn = t;
+            rsrc_t rAn = rA, rBn = rB;
+            int ldan = lda, ldbn = ldb;
+            if (work && it + 1 < ntl) {
+                tn = ws_tile(ga, tile_id(it + 1));
+                rsrcs(tn, rAn, rBn, ldan, ldbn);
+            }
+            if (work) {
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+            }
+            for (int kt = 0; kt < nph; ++kt) {
+                if (work && kt < nk) {
+                    const float* Ac = (kt & 1) ? As1 : As0;
+                    const float* Bc = (kt & 1) ? Bs1 : Bs0;
+                    const bool last = kt + 1 == nk;
+                    // prefetch: the next slice, or after the last one the next tile's slice 0
+                    // (the last tile re-reads a valid slice: no branch around the loads)
+                    if (!last) {
+#pragma unroll
+                        for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, true>(rA, lda, p, t.i0, (kt + 1) * BK);
+#pragma unroll
+                        for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, true>(rB, ldb, p, t.j0, (kt + 1) * BK);
+                    } else {
+#pragma unroll
+                        for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, true>(rAn, ldan, p, tn.i0, 0);
+#pragma unroll
+                        for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, true>(rBn, ldbn, p, tn.j0, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    float av[8], bv[8][2];
+                    {
+                        const float* r = Ac + (wi + l32) * RP + 8 * lh;
+                        const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
+                        av[0] = x0.x; av[1] = x0.y; av[2] = x0.z; av[3] = x0.w;
+                        av[4] = x1.x; av[5] = x1.y; av[6] = x1.z; av[7] = x1.w;
+                    }
+#pragma unroll
+                    for (int b = 0; b < 2; ++b) {
+                        const float* r = Bc + (wj + b * 32 + l32) * RP + 8 * lh;
+                        const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
+                        bv[0][b] = x0.x; bv[1][b] = x0.y; bv[2][b] = x0.z; bv[3][b] = x0.w;
+                        bv[4][b] = x1.x; bv[5][b] = x1.y; bv[6][b] = x1.z; bv[7][b] = x1.w;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+                        for (int b = 0; b < 2; ++b)
+                            acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk][b], acc[b], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    float* An = (kt & 1) ? As0 : As1;
+                    float* Bn = (kt & 1) ? Bs0 : Bs1;
+#pragma unroll
+                    for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, true, RP>(An, p, ra[p]);
+#pragma unroll
+                    for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, true, RP>(Bn, p, rb[p]);
+                }
+                ws_barrier();
+            }
+            // period boundary: the gradient tile to LDS (O finished the previous one's reads
+            // before the last phase barrier)
+            if (work) {
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        Gt[(wi + (r & 3) + 8 * (r >> 2) + 4 * lh) * PT + wj + b * 32 + l32] = acc[b][r];
+            }
+            ws_barrier();
+            t = tn;
+            rA = rAn; rB = rBn; lda = ldan; ldb = ldbn;
+        }
+        return;
+    }
+
+    // ------------------------------------------------------------ O: the optimiser
+    const int otid = threadIdx.x - 256, ow = wave - 4;
+    constexpr int TPR = BN / 4;  // 32 threads per row, 8 rows per unit
+    const int cj = (otid % TPR) * 4, ri = otid / TPR;
+    const float lr = e.lr, tau = e.tau;
+    // per-tile state of the tile being optimised
+    struct Res {
+        rsrc_t rP, rPo, rM, rV, rT;
+    };
+    auto tile_res = [&](const WsTile& tt, Res& rs, bool& hasT, int& gM, int& ldc) {
+        const GemmArgs& g = ga.g[tt.gi];
+        gM = uni(g.M);
+        ldc = uni(g.ldc);
+        const long long pb = uni64((long long)tt.slot * e.P + e.w_off[tt.gi] + (long long)tt.y * e.ens);
+        const long long nleaf = (long long)gM * ldc;
+        rs.rP = make_rsrc(e.p_in + pb, nleaf);
+        rs.rPo = make_rsrc(e.p_out + pb, nleaf);
+        rs.rM = make_rsrc(e.m + pb, nleaf);
+        rs.rV = make_rsrc(e.v + pb, nleaf);
+        hasT = e.target != nullptr;
+        rs.rT = make_rsrc(uniptr(hasT ? e.target + (long long)tt.slot * e.PT + e.w_off[tt.gi] + (long long)tt.y * e.ens
+                                      : e.m + pb), nleaf);
+    };
+    float4 p4[3], m4[3], v4[3], t4[3];
+    auto issue = [&](const Res& rs, bool hasT, int ldc, int i0, int j0, int u, int q) {
+        const int off = ((i0 + u * 8 + ri) * ldc + j0 + cj) * 4;
+        p4[q] = bload4_aux(rs.rP, off, 0);
+        m4[q] = bload4_aux(rs.rM, off, 1);
+        v4[q] = bload4_aux(rs.rV, off, 1);
+        t4[q] = hasT ? bload4_aux(rs.rT, off, 1) : float4{0.f, 0.f, 0.f, 0.f};
+    };
+    WsTile t = ws_tile(ga, tile_id(0));
+    Res rs;
+    bool hasT;
+    int gM, ldc;
+    tile_res(t, rs, hasT, gM, ldc);
+    ws_barrier();  // G's prologue barrier
+    for (int it = 0; it <= ntl; ++it) {
+        if (it >= 1) {
+            // tile it - 1 (its gradient is in Gt; units 0 and 1 were issued at the last boundary)
+            const float tc = (float)(e.count[t.slot] + 1);
+            const float bc1 = 1.0f - powf(0.9f, tc), bc2 = 1.0f - powf(0.999f, tc);
+            const float rbc1 = 1.0f / bc1, rbc2 = 1.0f / bc2;
+            const int rows = min(BM, gM - t.i0);
+            float mx = -INFINITY, mn = INFINITY, ss = 0.f;
+#pragma unroll
+            for (int u = 0; u < WS_NU; ++u) {
+                // unit u: row 8 u + ri, columns cj .. cj + 3 (adam_epilogue's per-thread order)
+                const int q = u % 3;
+                if (u + 2 < WS_NU) issue(rs, hasT, ldc, t.i0, t.j0, u + 2, (u + 2) % 3);
+                const int i = u * 8 + ri;
+                const int off = ((t.i0 + i) * ldc + t.j0 + cj) * 4;
+                const bool live = i < rows;
+                float* gs = Gt + i * PT + cj;
+                float pp[4] = {p4[q].x, p4[q].y, p4[q].z, p4[q].w};
+                float mm[4] = {m4[q].x, m4[q].y, m4[q].z, m4[q].w};
+                float vv[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
+                float tt[4] = {t4[q].x, t4[q].y, t4[q].z, t4[q].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float gr = gs[c];
+                    mm[c] = 0.1f * gr + 0.9f * mm[c];
+                    vv[c] = 0.001f * (gr * gr) + 0.999f * vv[c];
+                    const float mh = mm[c] * rbc1, vh = vv[c] * rbc2;
+                    tt[c] = tau * pp[c] + (1.0f - tau) * tt[c];
+                    pp[c] = pp[c] + (-lr) * (mh * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vh) + 1e-8f));
+                    gs[c] = pp[c];
+                    mx = live ? fmaxf(mx, gr) : mx;
+                    mn = live ? fminf(mn, gr) : mn;
+                    ss = live ? ss + gr * gr : ss;
+                }
+                bstore4_aux(rs.rPo, float4{pp[0], pp[1], pp[2], pp[3]}, off, 0);
+                bstore4_aux(rs.rM, float4{mm[0], mm[1], mm[2], mm[3]}, off, 1);
+                bstore4_aux(rs.rV, float4{vv[0], vv[1], vv[2], vv[3]}, off, 1);
+                if (hasT) bstore4_aux(rs.rT, float4{tt[0], tt[1], tt[2], tt[3]}, off, 1);
+                // the stats chains are folded in this unit (the compiler otherwise sinks them
+                // past the barriers and keeps every unit's gradient values live: 72 spilled VGPRs)
+                asm volatile("" : "+v"(mx), "+v"(mn), "+v"(ss));
+                if (u + 1 == WS_NU) {
+                    // the tile's grad stats: per wave, then the 4 O waves through red[] (read
+                    // after the next barrier)
+                    mx = wave_max(mx);
+                    mn = wave_min(mn);
+                    ss = wave_sum(ss);
+                    if ((otid & 63) == 0) {
+                        red[ow] = mx;
+                        red[4 + ow] = mn;
+                        red[8 + ow] = ss;
+                    }
+                }
+                ws_barrier();
+            }
+            if (otid == 0) {
+                float* st = e.stats + ((long long)t.slot * e.n_total_chunks + e.stat_base[t.gi] + t.y * t.per + t.tile) * 3;
+                st[0] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+                st[1] = fminf(fminf(red[4], red[5]), fminf(red[6], red[7]));
+                st[2] = red[8] + red[9] + red[10] + red[11];
+            }
+            // W^T[j][i0 .. i0 + BM) as float4 runs along i (hidden layers: M = H, full tiles)
+            const bool wt = e.wt_off[t.gi] >= 0;
+            float* __restrict__ WT = wt ? e.wt_out + (long long)t.slot * e.PTT + e.wt_off[t.gi] + (long long)t.y * e.wt_sy
+                                        : nullptr;
+            for (int u = 0; u < WS_NU; ++u) {
+                if (wt) {
+                    // (the lane index through an opaque copy: per-unit addresses are computed here,
+                    // not hoisted to the kernel top and spilled)
+                    constexpr int TPC = BM / 4;
+                    const int qq = opq(otid) + 256 * u;
+                    const int jj = qq / TPC, ii = (qq % TPC) * 4;
+                    const float* src = Gt + ii * PT + jj;
+                    *reinterpret_cast<float4*>(WT + (long long)(t.j0 + jj) * gM + t.i0 + ii) =
+                        float4{src[0], src[PT], src[2 * PT], src[3 * PT]};
+                }
+                ws_barrier();
+            }
+        } else {
+            for (int u = 0; u < 2 * WS_NU; ++u) ws_barrier();
+        }
+        for (int kt = 2 * WS_NU; kt < nph; ++kt) ws_barrier();
+        // period boundary: the next tile's first units go in flight while G writes its gradient tile
+        if (it < ntl) {
+            t = ws_tile(ga, tile_id(it));
+            tile_res(t, rs, hasT, gM, ldc);
+            issue(rs, hasT, ldc, t.i0, t.j0, 0, 0);
+            issue(rs, hasT, ldc, t.i0, t.j0, 1, 1);
+        }
+        ws_barrier();
+    }
+}
+
 int gemm_group_tiles(int tile, int M, int N) {
     const int bm = (tile & 1) ? 128 : 64, bn = (tile & 2) ? 128 : 64;
     return ((M + bm - 1) / bm) * (N / bn);
@@ -713,6 +1125,16 @@ void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, c
     }
     ga.first[ng] = tot;
     ga.ng = ng;
+    if (adam && tile == 14) {
+        // wave-specialised persistent launch: 2 blocks per CU over the tiles, then the
+        // small-leaf blocks
+        ga.adam = *adam;
+        const int want = adam->persist > 0 ? adam->persist : 512, cap = 8 * ((tot + 7) / 8);
+        const int per = want < cap ? want : cap;
+        ga.adam.persist = per;
+        hipLaunchKernelGGL(dwopt_ws_kernel, dim3(per + adam->small_blocks), dim3(512), 0, s, ga);
+        return;
+    }
     if (adam) {
         ga.adam = *adam;
         tot += adam->small_blocks;

@@ -91,8 +91,8 @@ const EngineOptionRef kEngineOptions[] = {
     {"stream_bwd", &EngineOptions::stream_bwd, 0, 1},   {"fused_adam", &EngineOptions::fused_adam, 0, 1},
     {"cdw_sb", &EngineOptions::cdw_sb, 0, 1},           {"serial", &EngineOptions::serial, 0, 1},
     {"streams", &EngineOptions::streams, 3, 4},         {"prio", &EngineOptions::prio, 0, 2},
-    {"dw_tile_critic", &EngineOptions::dw_tile_critic, 0, 10},
-    {"dw_tile_actor", &EngineOptions::dw_tile_actor, 0, 10},
+    {"dw_tile_critic", &EngineOptions::dw_tile_critic, 0, 14},
+    {"dw_tile_actor", &EngineOptions::dw_tile_actor, 0, 14},
     {"adam_nt", &EngineOptions::adam_nt, 0, 3},
     {"dw_stagger", &EngineOptions::dw_stagger, 0, 256},
 };
