@@ -58,15 +58,8 @@ DEV float wave_min(float v) {
     return v;
 }
 
-// Sum over the 4 lanes l, l^16, l^32, l^48 (the lk index of the streamed kernels' lane
-// layout), every lane getting the sum: v_permlane16_swap / v_permlane32_swap (VALU, no
-// LDS traffic and no per-lane ds_bpermute address to keep live; __shfl_xor's addresses
-// were the spilled registers of the LN backward).  The same additions as
-// v += shfl_xor(v, 16); v += shfl_xor(v, 32) (fp add is commutative): bit-identical.
-// Inline asm: this compiler folds the two results of __builtin_amdgcn_permlane16_swap
-// into one when both inputs are the same value.  The s_nop covers the VALU-write ->
-// permlane-read hazard.
-// an opaque copy of v (the compiler cannot hoist what is computed from it)
+// an opaque copy of v (the compiler cannot hoist what is computed from it; dwopt_ws_kernel's
+// per-unit W^T addresses)
 DEV int opq(int v) {
     asm volatile("" : "+v"(v));
     return v;
@@ -80,6 +73,14 @@ DEV int lane_id_asm() {
     return l;
 }
 
+// Sum over the 4 lanes l, l^16, l^32, l^48 (the lk index of the streamed kernels' lane
+// layout), every lane getting the sum: v_permlane16_swap / v_permlane32_swap (VALU, no
+// LDS traffic and no per-lane ds_bpermute address to keep live; __shfl_xor's addresses
+// were the spilled registers of the LN backward).  The same additions as
+// v += shfl_xor(v, 16); v += shfl_xor(v, 32) (fp add is commutative): bit-identical.
+// Inline asm: this compiler folds the two results of __builtin_amdgcn_permlane16_swap
+// into one when both inputs are the same value.  The s_nop covers the VALU-write ->
+// permlane-read hazard.
 DEV float lk_sum(float v) {
     float a = v, b = v;
     asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
@@ -1464,6 +1465,43 @@ DEV void ef_tail(f32x4 (&acc)[4], float4 a, const float* xs, int lk, int li) {
     acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b, acc[3], 0, 0, 0);
 }
 
+// The dX product dh^T = du^T W_l^T of the streamed backward reading W_l [k][j] itself (no W_l^T
+// copy).  The output layout is ef_kloop's (tile c, A row li = feature 64w + 4li + c); the
+// reduction index of k-step s = 4t + q is j = 16t + 4lk + q, so a lane's float4
+// W_l[64w + 4li + c][16t + 4lk .. +3] feeds tile c's MFMAs of the 4 k-steps of group t (a row
+// is read in 64-B runs: 4 lanes per row, 16 rows per load instruction).  ring[g][c] holds
+// group t0 + g of tile c; NG groups (4 NG k-steps) in flight, refilled across the layer
+// boundary from the next product's W (w_next) as ef_kloop's ring does.
+template <int NG>
+DEV void bw_kloop(f32x4 (&acc)[4], float4 (&ring)[NG][4], rsrc_t rW, const float* xs, int NTG, int w_cur,
+                  int w_next, int lo, int lk, int li) {
+    constexpr int NC = EF_NC, H = EF_H;
+    int t0 = 0;
+    do {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int t = t0 + g;
+            float b[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[q] = xs[(16 * t + 4 * lk + q) * NC + li];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float av[4] = {ring[g][0][q], ring[g][1][q], ring[g][2][q], ring[g][3][q]};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c], b[q], acc[c], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // refill: group t + NG of this product, or group t + NG - NTG of the next one
+            const int base = t + NG < NTG ? w_cur + 16 * (t + NG) : w_next + 16 * (t + NG - NTG);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) ring[g][c] = bload4(rW, base + lo + c * H);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        t0 += NG;
+    } while (t0 < NTG);
+}
+
 bool euler_flow_supported(int H, int L, int D, int A, int B) {
     return H == EF_H && L >= 1 && L <= EF_MAX_LAYERS && D + A + 1 <= EF_K0MAX && A <= 8 && B % EF_NC == 0;
 }
@@ -2277,9 +2315,12 @@ bool stream_bwd_supported(int H, int L, int nout, int M, int Mg) {
            Mg % EF_NC == 0 && Mg <= M;
 }
 
-template <bool LN>
+template <bool LN, bool WD = false>
 __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(const StreamBwdArgs g) {
     constexpr int H = EF_H, NC = EF_NC, NT = EF_NW * 64, PF = sb_pf<LN>();
+    // WD (actor nets): the dX products read W_l directly (bw_kloop), 2 groups of 4 k-steps in flight
+    static_assert(!(WD && LN), "W-direct backward: actor (no LayerNorm) variant only");
+    constexpr int NG = 2;
     __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];  // du_l [H][NC] (+ look-ahead slack)
     __shared__ __attribute__((aligned(16))) float scr[H * NC];         // head kernel W_L [H][nout]; then LN-grad products
     __shared__ float colred[2][EF_NW][NC];                            // LN column-stat partials per wave
@@ -2350,11 +2391,23 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
     // waited for the ring refills of the next product, every layer)
     const int lo = lk * H + 64 * w + 4 * li;
     float4 ring[PF];
+    // W-direct: lane offset of W_l[64w + 4li][4lk] (tile c: + c H, group t: + 16 t)
+    const int lo_w = (64 * w + 4 * li) * H + 4 * lk;
+    const rsrc_t rWd = make_rsrc(P, g.ens);
+    float4 ringw[WD ? NG : 1][4];
     auto load_first = [&]() {
         load_epi(L - 1, tid, li, lk);
-        const int wf = L > 1 ? (int)g.wt_off[L - 1] : 0;
+        if constexpr (WD) {
+            const int wf = L > 1 ? (int)g.w_off[L - 1] : 0;
 #pragma unroll
-        for (int p = 0; p < PF; ++p) ring[p] = bload4(rT, wf + 4 * p * H + lo);
+            for (int gg = 0; gg < NG; ++gg)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) ringw[gg][c] = bload4(rWd, wf + 16 * gg + lo_w + c * H);
+        } else {
+            const int wf = L > 1 ? (int)g.wt_off[L - 1] : 0;
+#pragma unroll
+            for (int p = 0; p < PF; ++p) ring[p] = bload4(rT, wf + 4 * p * H + lo);
+        }
     };
     // lane layout (as ef_kloop's accumulators): column li, features f = 64w + 16lk + 4r + c
     // last hidden layer: dh = W_L dout (nout <= 8, VALU)
@@ -2577,8 +2630,14 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         f32x4 acc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int wn = (int)g.wt_off[l >= 2 ? l - 1 : l];  // next product's W^T (l-1 >= 1), else a harmless re-load
-        ef_kloop<PF>(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lk_l * H + 64 * w + 4 * li_l, lk_l, li_l);
+        if constexpr (WD) {
+            const int wn = (int)g.w_off[l >= 2 ? l - 1 : l];  // next product's W (l-1 >= 1), else a harmless re-load
+            bw_kloop<NG>(acc, ringw, rWd, slab, H / 16, (int)g.w_off[l], wn, (64 * w + 4 * li_l) * H + 4 * lk_l, lk_l,
+                         li_l);
+        } else {
+            const int wn = (int)g.wt_off[l >= 2 ? l - 1 : l];  // next product's W^T (l-1 >= 1), else a harmless re-load
+            ef_kloop<PF>(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lk_l * H + 64 * w + 4 * li_l, lk_l, li_l);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -2595,6 +2654,7 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
 void launch_stream_bwd(bool ln, const StreamBwdArgs& a, hipStream_t s) {
     const dim3 grid((a.M / EF_NC) * a.ny * a.nz), block(EF_NW * 64);
     if (ln) hipLaunchKernelGGL((stream_bwd_kernel<true>), grid, block, 0, s, a);
+    else if (a.wdirect) hipLaunchKernelGGL((stream_bwd_kernel<false, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((stream_bwd_kernel<false>), grid, block, 0, s, a);
 }
 
