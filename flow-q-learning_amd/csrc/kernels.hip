@@ -89,7 +89,9 @@ DEV float lk_sum(float v) {
     return s + c;
 }
 
-// Block-wide reductions for 256-thread blocks; `red` needs 4 floats.
+// Block-wide reductions over the first 4 waves (256 threads); `red` needs one float per
+// wave.  In a 512-thread block the other waves only join the barriers (their values are
+// ignored), so the result is the 256-thread one, bit for bit.
 DEV float block_sum(float v, float* red) {
     v = wave_sum(v);
     const int w = threadIdx.x >> 6;
@@ -135,68 +137,94 @@ DEV int xcd_remap(int bid, int total) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
 }
 
+// optax.adam moments and the target EMA of one element, every rounding step explicit (fp
+// contraction off, fmaf where a fused multiply-add is meant): the kernels that run the
+// optimiser (adam_chunk, the fused dW epilogue, the wave-specialised launch) then give
+// bit-identical results whatever the surrounding code lets the compiler fuse.
+DEV void adam_moments(float g, float& m, float& v) {
+#pragma clang fp contract(off)
+    m = fmaf(0.1f, g, 0.9f * m);
+    v = fmaf(0.001f, g * g, 0.999f * v);
+}
+DEV float ema_target(float p, float t, float tau) {
+#pragma clang fp contract(off)
+    return fmaf(tau, p, (1.0f - tau) * t);
+}
+// the fused epilogues' step: bias corrections by reciprocal, the step by v_sqrt + v_rcp
+// (<= 2 ulp from optax's IEEE divisions)
+DEV float adam_step_fast(float p, float m, float v, float rbc1, float rbc2, float lr) {
+#pragma clang fp contract(off)
+    const float mh = m * rbc1, vh = v * rbc2;
+    return fmaf(-lr, mh * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vh) + 1e-8f), p);
+}
+// adam_chunk's step: IEEE divisions, as optax
+DEV float adam_step_ieee(float p, float m, float v, float bc1, float bc2, float lr) {
+#pragma clang fp contract(off)
+    const float mh = m / bc1, vh = v / bc2;
+    return fmaf(-lr, mh / (sqrtf(vh) + 1e-8f), p);
+}
+
 // optax.adam (b1 .9, b2 .999, eps 1e-8 outside the sqrt, bias correction with
 // count+1) + target EMA from the pre-update critic + per-chunk grad stats, one
-// chunk of one member per 256-thread block (adam_kernel; and the small-leaf
-// blocks of the fused dW launch).
-DEV void adam_chunk(const AdamArgs& a, int bx, int z) {
+// chunk of one member per block (adam_kernel; and the small-leaf blocks of the fused dW
+// launch).  NT-thread blocks: threads 0..255 do the work, the others only join the
+// barriers (the wave-specialised launch has 512), so the results do not depend on NT.
+template <int NT>
+DEV void adam_chunk_t(const AdamArgs& a, int bx, int z) {
     const int ci = a.ids ? a.ids[bx] : a.chunk_base + bx;
     const int slot = a.slots[z];
     const Chunk ck = a.chunks[ci];
     const long long base = (long long)slot * a.P + a.net_off + ck.off;
-    const float* __restrict__ Pin = a.p_in + base;
-    float* __restrict__ P = a.p_out + base;
-    const float* __restrict__ G = a.g + base;
-    float* __restrict__ Mm = a.m + base;
-    float* __restrict__ V = a.v + base;
-    float* __restrict__ T = a.target ? a.target + (long long)slot * a.PT + ck.off : nullptr;
     const float t = (float)(a.count[slot] + 1);
     const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
     float mx = -INFINITY, mn = INFINITY, ss = 0.f;
     const float lr = a.lr, tau = a.tau;
-    // one Adam element (+ EMA of the target from the pre-update value)
-#define FQ_ADAM1(g, p, m, v, hasT, tp)                              \
-    do {                                                            \
-        m = 0.1f * (g) + 0.9f * m;                                  \
-        v = 0.001f * ((g) * (g)) + 0.999f * v;                      \
-        const float mh_ = m / bc1, vh_ = v / bc2;                   \
-        if (hasT) tp = tau * p + (1.0f - tau) * tp;                 \
-        p = p + (-lr) * (mh_ / (sqrtf(vh_) + 1e-8f));               \
-        mx = fmaxf(mx, (g));                                        \
-        mn = fminf(mn, (g));                                        \
-        ss += (g) * (g);                                            \
-    } while (0)
-    const bool hasT = T != nullptr;
-    if ((ck.len & 3) == 0) {
-        for (int i = threadIdx.x * 4; i < ck.len; i += 1024) {
-            const float4 g4 = *reinterpret_cast<const float4*>(G + i);
-            float4 p4 = *reinterpret_cast<const float4*>(Pin + i);
-            float4 m4 = *reinterpret_cast<float4*>(Mm + i);
-            float4 v4 = *reinterpret_cast<float4*>(V + i);
-            float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (hasT) t4 = *reinterpret_cast<float4*>(T + i);
-            FQ_ADAM1(g4.x, p4.x, m4.x, v4.x, hasT, t4.x);
-            FQ_ADAM1(g4.y, p4.y, m4.y, v4.y, hasT, t4.y);
-            FQ_ADAM1(g4.z, p4.z, m4.z, v4.z, hasT, t4.z);
-            FQ_ADAM1(g4.w, p4.w, m4.w, v4.w, hasT, t4.w);
-            *reinterpret_cast<float4*>(P + i) = p4;
-            *reinterpret_cast<float4*>(Mm + i) = m4;
-            *reinterpret_cast<float4*>(V + i) = v4;
-            if (hasT) *reinterpret_cast<float4*>(T + i) = t4;
-        }
-    } else {
-        for (int i = threadIdx.x; i < ck.len; i += 256) {
-            const float gv = G[i];
-            float p = Pin[i], m = Mm[i], v = V[i], tv = hasT ? T[i] : 0.f;
-            FQ_ADAM1(gv, p, m, v, hasT, tv);
-            P[i] = p;
-            Mm[i] = m;
-            V[i] = v;
-            if (hasT) T[i] = tv;
+    const bool hasT = a.target != nullptr;
+    if (NT == 256 || threadIdx.x < 256) {
+        const float* __restrict__ Pin = a.p_in + base;
+        float* __restrict__ P = a.p_out + base;
+        const float* __restrict__ G = a.g + base;
+        float* __restrict__ Mm = a.m + base;
+        float* __restrict__ V = a.v + base;
+        float* __restrict__ T = hasT ? a.target + (long long)slot * a.PT + ck.off : nullptr;
+        auto one = [&](float g, float& p, float& m, float& v, float& tp) {
+            adam_moments(g, m, v);
+            if (hasT) tp = ema_target(p, tp, tau);
+            p = adam_step_ieee(p, m, v, bc1, bc2, lr);
+            mx = fmaxf(mx, g);
+            mn = fminf(mn, g);
+            ss = fmaf(g, g, ss);
+        };
+        if ((ck.len & 3) == 0) {
+            for (int i = threadIdx.x * 4; i < ck.len; i += 1024) {
+                const float4 g4 = *reinterpret_cast<const float4*>(G + i);
+                float4 p4 = *reinterpret_cast<const float4*>(Pin + i);
+                float4 m4 = *reinterpret_cast<float4*>(Mm + i);
+                float4 v4 = *reinterpret_cast<float4*>(V + i);
+                float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (hasT) t4 = *reinterpret_cast<float4*>(T + i);
+                one(g4.x, p4.x, m4.x, v4.x, t4.x);
+                one(g4.y, p4.y, m4.y, v4.y, t4.y);
+                one(g4.z, p4.z, m4.z, v4.z, t4.z);
+                one(g4.w, p4.w, m4.w, v4.w, t4.w);
+                *reinterpret_cast<float4*>(P + i) = p4;
+                *reinterpret_cast<float4*>(Mm + i) = m4;
+                *reinterpret_cast<float4*>(V + i) = v4;
+                if (hasT) *reinterpret_cast<float4*>(T + i) = t4;
+            }
+        } else {
+            for (int i = threadIdx.x; i < ck.len; i += 256) {
+                const float gv = G[i];
+                float p = Pin[i], m = Mm[i], v = V[i], tv = hasT ? T[i] : 0.f;
+                one(gv, p, m, v, tv);
+                P[i] = p;
+                Mm[i] = m;
+                V[i] = v;
+                if (hasT) T[i] = tv;
+            }
         }
     }
-#undef FQ_ADAM1
-    __shared__ float red[4];
+    __shared__ float red[NT / 64];
     mx = block_max(mx, red);
     mn = block_min(mn, red);
     ss = block_sum(ss, red);
@@ -207,6 +235,7 @@ DEV void adam_chunk(const AdamArgs& a, int bx, int z) {
         st[2] = ss;
     }
 }
+DEV void adam_chunk(const AdamArgs& a, int bx, int z) { adam_chunk_t<256>(a, bx, z); }
 
 
 // =============================================================== GEMM ======
@@ -419,17 +448,15 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     const float gr = gs[c];
-                    mm[c] = 0.1f * gr + 0.9f * mm[c];
-                    vv[c] = 0.001f * (gr * gr) + 0.999f * vv[c];
                     // bias corrections by reciprocal and the step by v_sqrt + v_rcp: <= 2 ulp from
                     // optax's IEEE divisions, and 3 IEEE division sequences fewer per element
-                    const float mh = mm[c] * rbc1, vh = vv[c] * rbc2;
-                    tt[c] = tau * pp[c] + (1.0f - tau) * tt[c];
-                    pp[c] = pp[c] + (-lr) * (mh * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vh) + 1e-8f));
+                    adam_moments(gr, mm[c], vv[c]);
+                    tt[c] = ema_target(pp[c], tt[c], tau);
+                    pp[c] = adam_step_fast(pp[c], mm[c], vv[c], rbc1, rbc2, lr);
                     gs[c] = pp[c];
                     mx = live ? fmaxf(mx, gr) : mx;
                     mn = live ? fminf(mn, gr) : mn;
-                    ss = live ? ss + gr * gr : ss;
+                    ss = live ? fmaf(gr, gr, ss) : ss;
                 }
                 bstore4_aux(rPo, float4{pp[0], pp[1], pp[2], pp[3]}, off, 0);
                 bstore4_aux(rM, float4{mm[0], mm[1], mm[2], mm[3]}, off, 1);
@@ -742,112 +769,13 @@ DEV WsTile ws_tile(const GemmGroupArgs& ga, int lt) {
     return t;
 }
 
-// block-level sums over 8 waves where waves 4-7 contribute the identity: the same value (and
-// bits) as block_sum over waves 0-3
-DEV float ws_block_sum(float v, float* red) {
-    v = wave_sum(v);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    return red[0] + red[1] + red[2] + red[3];
-}
-DEV float ws_block_max(float v, float* red) {
-    v = wave_max(v);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-}
-DEV float ws_block_min(float v, float* red) {
-    v = wave_min(v);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    return fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
-}
-
-// adam_chunk for a 512-thread block: threads 0..255 do exactly adam_chunk's work (same
-// per-thread order, same reduction order), threads 256..511 only join the barriers
-DEV void adam_chunk_ws(const AdamArgs& a, int bx, int z) {
-    const int ci = a.ids ? a.ids[bx] : a.chunk_base + bx;
-    const int slot = a.slots[z];
-    const Chunk ck = a.chunks[ci];
-    const long long base = (long long)slot * a.P + a.net_off + ck.off;
-    const float t = (float)(a.count[slot] + 1);
-    const float bc1 = 1.0f - powf(0.9f, t), bc2 = 1.0f - powf(0.999f, t);
-    float mx = -INFINITY, mn = INFINITY, ss = 0.f;
-    const float lr = a.lr, tau = a.tau;
-    const bool hasT = a.target != nullptr;
-    if (threadIdx.x < 256) {
-        const float* __restrict__ Pin = a.p_in + base;
-        float* __restrict__ P = a.p_out + base;
-        const float* __restrict__ G = a.g + base;
-        float* __restrict__ Mm = a.m + base;
-        float* __restrict__ V = a.v + base;
-        float* __restrict__ T = hasT ? a.target + (long long)slot * a.PT + ck.off : nullptr;
-#define FQ_ADAM1(g, p, m, v, hasT, tp)                              \
-    do {                                                            \
-        m = 0.1f * (g) + 0.9f * m;                                  \
-        v = 0.001f * ((g) * (g)) + 0.999f * v;                      \
-        const float mh_ = m / bc1, vh_ = v / bc2;                   \
-        if (hasT) tp = tau * p + (1.0f - tau) * tp;                 \
-        p = p + (-lr) * (mh_ / (sqrtf(vh_) + 1e-8f));               \
-        mx = fmaxf(mx, (g));                                        \
-        mn = fminf(mn, (g));                                        \
-        ss += (g) * (g);                                            \
-    } while (0)
-        if ((ck.len & 3) == 0) {
-            for (int i = threadIdx.x * 4; i < ck.len; i += 1024) {
-                const float4 g4 = *reinterpret_cast<const float4*>(G + i);
-                float4 p4 = *reinterpret_cast<const float4*>(Pin + i);
-                float4 m4 = *reinterpret_cast<float4*>(Mm + i);
-                float4 v4 = *reinterpret_cast<float4*>(V + i);
-                float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (hasT) t4 = *reinterpret_cast<float4*>(T + i);
-                FQ_ADAM1(g4.x, p4.x, m4.x, v4.x, hasT, t4.x);
-                FQ_ADAM1(g4.y, p4.y, m4.y, v4.y, hasT, t4.y);
-                FQ_ADAM1(g4.z, p4.z, m4.z, v4.z, hasT, t4.z);
-                FQ_ADAM1(g4.w, p4.w, m4.w, v4.w, hasT, t4.w);
-                *reinterpret_cast<float4*>(P + i) = p4;
-                *reinterpret_cast<float4*>(Mm + i) = m4;
-                *reinterpret_cast<float4*>(V + i) = v4;
-                if (hasT) *reinterpret_cast<float4*>(T + i) = t4;
-            }
-        } else {
-            for (int i = threadIdx.x; i < ck.len; i += 256) {
-                const float gv = G[i];
-                float p = Pin[i], m = Mm[i], v = V[i], tv = hasT ? T[i] : 0.f;
-                FQ_ADAM1(gv, p, m, v, hasT, tv);
-                P[i] = p;
-                Mm[i] = m;
-                V[i] = v;
-                if (hasT) T[i] = tv;
-            }
-        }
-#undef FQ_ADAM1
-    }
-    __shared__ float red[8];
-    mx = ws_block_max(mx, red);
-    mn = ws_block_min(mn, red);
-    ss = ws_block_sum(ss, red);
-    if (threadIdx.x == 0) {
-        float* st = a.stats + ((long long)slot * a.n_total_chunks + ci) * 3;
-        st[0] = mx;
-        st[1] = mn;
-        st[2] = ss;
-    }
-}
-
 __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga) {
     __shared__ __attribute__((aligned(16))) float smem[WS_SMEM];
     constexpr int BM = WS_BM, BN = WS_BN, BK = WS_BK, RP = WS_RP, PT = WS_PT;
     const int nper = ga.adam.persist;  // persistent blocks (a multiple of 8)
     if ((int)blockIdx.x >= nper) {
         const int sb = blockIdx.x - nper, nch = ga.adam.small.n_chunks;
-        adam_chunk_ws(ga.adam.small, sb % nch, sb / nch);
+        adam_chunk_t<512>(ga.adam.small, sb % nch, sb / nch);
         return;
     }
     const int T = ga.first[ga.ng];
@@ -1042,15 +970,13 @@ __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     const float gr = gs[c];
-                    mm[c] = 0.1f * gr + 0.9f * mm[c];
-                    vv[c] = 0.001f * (gr * gr) + 0.999f * vv[c];
-                    const float mh = mm[c] * rbc1, vh = vv[c] * rbc2;
-                    tt[c] = tau * pp[c] + (1.0f - tau) * tt[c];
-                    pp[c] = pp[c] + (-lr) * (mh * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vh) + 1e-8f));
+                    adam_moments(gr, mm[c], vv[c]);
+                    tt[c] = ema_target(pp[c], tt[c], tau);
+                    pp[c] = adam_step_fast(pp[c], mm[c], vv[c], rbc1, rbc2, lr);
                     gs[c] = pp[c];
                     mx = live ? fmaxf(mx, gr) : mx;
                     mn = live ? fminf(mn, gr) : mn;
-                    ss = live ? ss + gr * gr : ss;
+                    ss = live ? fmaf(gr, gr, ss) : ss;
                 }
                 bstore4_aux(rs.rPo, float4{pp[0], pp[1], pp[2], pp[3]}, off, 0);
                 bstore4_aux(rs.rM, float4{mm[0], mm[1], mm[2], mm[3]}, off, 1);

@@ -79,6 +79,7 @@ struct EngineOptions {
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
     int dw_stagger = 0;    // fused dW + optimiser: first-wave start offsets (AdamEpi::stagger)
     int bwd_wdirect = 0;   // actor backwards read W_l directly: no W^T copies of the actor nets
+    int dw_persist = 0;    // tile 14: persistent blocks of the wave-specialised launch (0: 2 per CU)
 };
 EngineOptions g_engine_opts;
 
@@ -97,6 +98,7 @@ const EngineOptionRef kEngineOptions[] = {
     {"adam_nt", &EngineOptions::adam_nt, 0, 3},
     {"dw_stagger", &EngineOptions::dw_stagger, 0, 256},
     {"bwd_wdirect", &EngineOptions::bwd_wdirect, 0, 1},
+    {"dw_persist", &EngineOptions::dw_persist, 0, 1 << 20},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -777,6 +779,7 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
             // (+1.0 % same-box; engine option adam_nt: bit mask, see AdamEpi::nt)
             ae.nt = h->opt.adam_nt;
             ae.stagger = h->opt.dw_stagger;
+            ae.persist = h->opt.dw_persist;
         }
         ae.small = adam_args(c, ni);
         ae.small_blocks = ae.small.n_chunks * c.nz;

@@ -330,7 +330,8 @@ def _sampled_run_now(H, B, steps):
     return out
 
 
-@pytest.mark.parametrize("H,B,tile", [(512, 256, 6), (256, 64, 6), (512, 256, 14), (256, 64, 14), (512, 1024, 14)])
+# (the fused dW + optimiser runs at H = 512 only: the streamed backward needs it)
+@pytest.mark.parametrize("H,B,tile", [(512, 256, 6), (512, 64, 6), (512, 256, 14), (512, 64, 14), (512, 1024, 14)])
 def test_fused_dw_optimiser_variants_bit_identical(H, B, tile):
     """The fused dW + optimiser launch at 4 blocks per CU (tile 10, the default), at 3
     (tile 6) and the wave-specialised persistent launch (tile 14: MFMA waves on tile n
