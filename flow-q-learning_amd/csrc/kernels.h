@@ -233,7 +233,6 @@ struct StreamBwdArgs {
     // [0] start, [1] end, then per layer pass (L-1-l): top, stats barrier in/out, slab barrier out,
     // product done
     unsigned long long* phase;
-    int wdirect;                          // 1: the dX products read W_l (params) instead of W_l^T (no LN only)
 };
 constexpr int SB_PHASE_STRIDE = 48;
 bool stream_bwd_supported(int H, int L, int nout, int M, int Mg);

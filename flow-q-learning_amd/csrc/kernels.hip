@@ -730,18 +730,19 @@ __global__ __launch_bounds__(256, 4) void gemm_group_kernel_o4(const GemmGroupAr
 // The same work as gemm_group_kernel_o4<64, 128, true, true, EPI_ADAM, 16> (tile id 14),
 // bit-identical, in a persistent launch whose blocks split their 8 waves into two groups
 // that run concurrently:
-//   G (waves 0-3): the dW k-loop of tile n (the same MFMA sequence as gemm_body, KB layout);
-//   O (waves 4-7): optax.adam / the target EMA / grad stats / the W^T copy of tile n-1, from
-//                  the gradient tile G left in LDS, with its p / m / v / target loads issued
-//                  two units ahead across the phase barriers.
-// A tile period is NPH = max(k-slices, 16) phases, each ending in one raw s_barrier that both
-// groups execute (no vmcnt(0): O's loads stay in flight across it); at the period boundary G
-// writes its accumulators into the gradient tile and one more barrier publishes it.  In the
+//   G (waves 0-3): the dW product of tile n, operand fragments loaded from L2 straight into
+//                  registers (no LDS staging, so no barrier inside the k-loop), the same MFMA
+//                  sequence as gemm_body's KB layout;
+//   O (waves 4-7): optax.adam / the target EMA / grad stats of tile n-1 and the W^T copy of
+//                  tile n-2, from gradient tiles G left in LDS (two buffers), with the p / m /
+//                  v / target loads of the next WS_D units always in flight (across tiles).
+// One tile period ends in two block barriers: A (both groups are done with the period's
+// LDS), then G writes its accumulators into gradient buffer n & 1, then B (published).  In the
 // one-tile-per-block launch every co-resident block ran its k-loop, then its HBM-bound
 // optimiser pass, at the same time as the others (they start together), so the two phases
-// hardly overlapped; here each CU has both kinds of work in flight all the time.
-constexpr int WS_BM = 64, WS_BN = 128, WS_BK = 16, WS_RP = 20, WS_PT = WS_BN + 1, WS_NU = 8;
-constexpr int WS_SMEM = 2 * (WS_BM + WS_BN) * WS_RP + WS_BM * WS_PT + 16;
+// hardly overlapped.
+constexpr int WS_BM = 64, WS_BN = 128, WS_BK = 16, WS_PT = WS_BN + 1, WS_NU = 8, WS_D = 3;
+constexpr int WS_SMEM = 2 * WS_BM * WS_PT + 32;
 
 DEV void ws_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
@@ -771,7 +772,7 @@ DEV WsTile ws_tile(const GemmGroupArgs& ga, int lt) {
 
 __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga) {
     __shared__ __attribute__((aligned(16))) float smem[WS_SMEM];
-    constexpr int BM = WS_BM, BN = WS_BN, BK = WS_BK, RP = WS_RP, PT = WS_PT;
+    constexpr int BM = WS_BM, BN = WS_BN, BK = WS_BK, PT = WS_PT, NU = WS_NU, D = WS_D;
     const int nper = ga.adam.persist;  // persistent blocks (a multiple of 8)
     if ((int)blockIdx.x >= nper) {
         const int sb = blockIdx.x - nper, nch = ga.adam.small.n_chunks;
@@ -787,124 +788,111 @@ __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga
     if (ntl == 0) return;
     auto tile_id = [&](int n) { return start + jb + n * nbx; };
     const int gK = uni(ga.g[0].K);  // one net: every problem has K = Mg
-    const int nk = (gK + BK - 1) / BK;
-    const int nph = nk > 2 * WS_NU ? nk : 2 * WS_NU;
-    float* const As0 = smem;
-    float* const Bs0 = smem + BM * RP;
-    float* const As1 = smem + (BM + BN) * RP;
-    float* const Bs1 = As1 + BM * RP;
-    float* const Gt = smem + 2 * (BM + BN) * RP;  // gradient tile [BM][PT], then the new p
-    float* const red = Gt + BM * PT;             // [12]: O-wave stats partials
+    const int nk = gK / BK;
+    float* const red = smem + 2 * BM * PT;  // [2][12]: O-wave stats partials of the last two tiles
     const AdamEpi& e = ga.adam;
     const int wave = threadIdx.x >> 6;
 
     if (wave < 4) {
-        // ------------------------------------------------------------ G: the k-loops
-        const int tid = threadIdx.x, lane = tid & 63;
+        // ------------------------------------------------------------ G: the dW products
+        const int lane = threadIdx.x & 63;
         const int wi = (wave >> 1) * (BM / 2), wj = (wave & 1) * (BN / 2);
         const int l32 = lane & 31, lh = lane >> 5;
-        constexpr int A_LD = BM * BK / 1024, B_LD = BN * BK / 1024;
-        float4 ra[A_LD], rb[B_LD];
-        f32x16 acc[2];
-        WsTile t = ws_tile(ga, tile_id(0));
-        auto rsrcs = [&](const WsTile& tt, rsrc_t& rA, rsrc_t& rB, int& lda, int& ldb) {
+        struct Src {
+            rsrc_t rA, rB;
+            int lda, ldb;
+        };
+        auto src = [&](const WsTile& tt) {
             const GemmArgs& g = ga.g[tt.gi];
             const int gM = uni(g.M), gN = uni(g.N);
-            lda = uni(g.lda);
-            ldb = uni(g.ldb);
-            rA = make_rsrc(uniptr(at(g.A, tt.slot, tt.y)), (long long)(gM - 1) * lda + gK);
-            rB = make_rsrc(uniptr(at(g.B, tt.slot, tt.y)), (long long)(gN - 1) * ldb + gK);
+            Src r;
+            r.lda = uni(g.lda);
+            r.ldb = uni(g.ldb);
+            r.rA = make_rsrc(uniptr(at(g.A, tt.slot, tt.y)), (long long)(gM - 1) * r.lda + gK);
+            r.rB = make_rsrc(uniptr(at(g.B, tt.slot, tt.y)), (long long)(gN - 1) * r.ldb + gK);
+            return r;
         };
-        rsrc_t rA, rB;
-        int lda, ldb;
-        rsrcs(t, rA, rB, lda, ldb);
-        // prologue: slice 0 of the first tile
+        // slice kt's fragments of this lane: A[i0 + wi + l32][16 kt + 8 lh .. +7] (the KB layout's
+        // k-blocked order: MFMA kk of lane half lh takes k = 8 lh + kk), B the same for columns
+        // j0 + wj + l32 and j0 + wj + 32 + l32 (rows past M read 0: buffer range)
+        auto load = [&](float4 (&f)[6], const Src& r, const WsTile& tt, int kt) {
+            const int k = kt * BK + 8 * lh;
+            const int oa = (tt.i0 + wi + l32) * r.lda + k;
+            const int ob0 = (tt.j0 + wj + l32) * r.ldb + k, ob1 = ob0 + 32 * r.ldb;
+            f[0] = bload4(r.rA, oa);
+            f[1] = bload4(r.rA, oa + 4);
+            f[2] = bload4(r.rB, ob0);
+            f[3] = bload4(r.rB, ob0 + 4);
+            f[4] = bload4(r.rB, ob1);
+            f[5] = bload4(r.rB, ob1 + 4);
+        };
+        // the MFMAs of one slice, in gemm_body's KB order (k = 8 lh + kk, column halves b = 0, 1)
+        auto slice = [&](f32x16 (&acc)[2], const float4 (&f)[6]) {
+            const float av[8] = {f[0].x, f[0].y, f[0].z, f[0].w, f[1].x, f[1].y, f[1].z, f[1].w};
+            const float bv0[8] = {f[2].x, f[2].y, f[2].z, f[2].w, f[3].x, f[3].y, f[3].z, f[3].w};
+            const float bv1[8] = {f[4].x, f[4].y, f[4].z, f[4].w, f[5].x, f[5].y, f[5].z, f[5].w};
 #pragma unroll
-        for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, true>(rA, lda, p, t.i0, 0);
-#pragma unroll
-        for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, true>(rB, ldb, p, t.j0, 0);
-#pragma unroll
-        for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, true, RP>(As0, p, ra[p]);
-#pragma unroll
-        for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, true, RP>(Bs0, p, rb[p]);
-        ws_barrier();
-        for (int it = 0; it <= ntl; ++it) {
-            const bool work = it < ntl;
-            // the slices' source: this tile, then in the last phase the next tile's slice 0
-            WsTile tn = t;
-            rsrc_t rAn = rA, rBn = rB;
-            int ldan = lda, ldbn = ldb;
-            if (work && it + 1 < ntl) {
-                tn = ws_tile(ga, tile_id(it + 1));
-                rsrcs(tn, rAn, rBn, ldan, ldbn);
+            for (int kk = 0; kk < 8; ++kk) {
+                acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv0[kk], acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv1[kk], acc[1], 0, 0, 0);
             }
-            if (work) {
+        };
+        WsTile t = ws_tile(ga, tile_id(0));
+        Src sr = src(t);
+        float4 cur[6], nxt[6];
+        load(cur, sr, t, 0);
+        for (int it = 0; it < ntl + 2; ++it) {  // + 2 periods: O's last Adam and W^T passes
+            f32x16 acc[2];
+            if (it < ntl) {
+                const bool more = it + 1 < ntl;
+                const WsTile tn = more ? ws_tile(ga, tile_id(it + 1)) : t;
+                const Src srn = more ? src(tn) : sr;
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-            }
-            for (int kt = 0; kt < nph; ++kt) {
-                if (work && kt < nk) {
-                    const float* Ac = (kt & 1) ? As1 : As0;
-                    const float* Bc = (kt & 1) ? Bs1 : Bs0;
-                    const bool last = kt + 1 == nk;
-                    // prefetch: the next slice, or after the last one the next tile's slice 0
-                    // (the last tile re-reads a valid slice: no branch around the loads)
-                    if (!last) {
-#pragma unroll
-                        for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, true>(rA, lda, p, t.i0, (kt + 1) * BK);
-#pragma unroll
-                        for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, true>(rB, ldb, p, t.j0, (kt + 1) * BK);
-                    } else {
-#pragma unroll
-                        for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, true>(rAn, ldan, p, tn.i0, 0);
-#pragma unroll
-                        for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, true>(rBn, ldbn, p, tn.j0, 0);
+                // two slices per trip, the fragment registers ping-ponged (a register copy of
+                // a prefetch would wait for it); nk is even (the launch checks K % 32 == 0)
+#if defined(FQ_WS_SKIP) && FQ_WS_SKIP == 1
+                for (int kt = 0; kt < 0; kt += 2) {
+#else
+                for (int kt = 0; kt < nk; kt += 2) {
+#endif
+                    load(nxt, sr, t, kt + 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    slice(acc, cur);
+                    __builtin_amdgcn_sched_barrier(0);
+                    // the slice after, or after the last one the next tile's first
+                    {  // selected, not branched: loads on both sides of a branch get
+                       // over-conservative vmcnt waits in the MFMAs after the join
+                        const bool in = kt + 2 < nk;
+                        Src sx;
+                        sx.rA = in ? sr.rA : srn.rA;
+                        sx.rB = in ? sr.rB : srn.rB;
+                        sx.lda = in ? sr.lda : srn.lda;
+                        sx.ldb = in ? sr.ldb : srn.ldb;
+                        WsTile tx = tn;
+                        tx.i0 = in ? t.i0 : tn.i0;
+                        tx.j0 = in ? t.j0 : tn.j0;
+                        load(cur, sx, tx, in ? kt + 2 : 0);
                     }
                     __builtin_amdgcn_sched_barrier(0);
-                    float av[8], bv[8][2];
-                    {
-                        const float* r = Ac + (wi + l32) * RP + 8 * lh;
-                        const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
-                        av[0] = x0.x; av[1] = x0.y; av[2] = x0.z; av[3] = x0.w;
-                        av[4] = x1.x; av[5] = x1.y; av[6] = x1.z; av[7] = x1.w;
-                    }
-#pragma unroll
-                    for (int b = 0; b < 2; ++b) {
-                        const float* r = Bc + (wj + b * 32 + l32) * RP + 8 * lh;
-                        const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
-                        bv[0][b] = x0.x; bv[1][b] = x0.y; bv[2][b] = x0.z; bv[3][b] = x0.w;
-                        bv[4][b] = x1.x; bv[5][b] = x1.y; bv[6][b] = x1.z; bv[7][b] = x1.w;
-                    }
+                    slice(acc, nxt);
                     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int kk = 0; kk < 8; ++kk)
-#pragma unroll
-                        for (int b = 0; b < 2; ++b)
-                            acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk][b], acc[b], 0, 0, 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    float* An = (kt & 1) ? As0 : As1;
-                    float* Bn = (kt & 1) ? Bs0 : Bs1;
-#pragma unroll
-                    for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, true, RP>(An, p, ra[p]);
-#pragma unroll
-                    for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, true, RP>(Bn, p, rb[p]);
                 }
-                ws_barrier();
+                t = tn;
+                sr = srn;
             }
-            // period boundary: the gradient tile to LDS (O finished the previous one's reads
-            // before the last phase barrier)
-            if (work) {
+            ws_barrier();  // A: O is done with gradient buffer it & 1 (its W^T pass of tile it - 2)
+            if (it < ntl) {
+                float* const Gt = smem + (it & 1) * BM * PT;
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
 #pragma unroll
                     for (int r = 0; r < 16; ++r)
                         Gt[(wi + (r & 3) + 8 * (r >> 2) + 4 * lh) * PT + wj + b * 32 + l32] = acc[b][r];
             }
-            ws_barrier();
-            t = tn;
-            rA = rAn; rB = rBn; lda = ldan; ldb = ldbn;
+            ws_barrier();  // B: gradient tile it published
         }
         return;
     }
@@ -914,55 +902,92 @@ __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga
     constexpr int TPR = BN / 4;  // 32 threads per row, 8 rows per unit
     const int cj = (otid % TPR) * 4, ri = otid / TPR;
     const float lr = e.lr, tau = e.tau;
-    // per-tile state of the tile being optimised
     struct Res {
         rsrc_t rP, rPo, rM, rV, rT;
+        int gM, ldc;
+        bool hasT;
     };
-    auto tile_res = [&](const WsTile& tt, Res& rs, bool& hasT, int& gM, int& ldc) {
+    auto tile_res = [&](const WsTile& tt) {
         const GemmArgs& g = ga.g[tt.gi];
-        gM = uni(g.M);
-        ldc = uni(g.ldc);
+        Res rs;
+        rs.gM = uni(g.M);
+        rs.ldc = uni(g.ldc);
         const long long pb = uni64((long long)tt.slot * e.P + e.w_off[tt.gi] + (long long)tt.y * e.ens);
-        const long long nleaf = (long long)gM * ldc;
+        const long long nleaf = (long long)rs.gM * rs.ldc;
         rs.rP = make_rsrc(e.p_in + pb, nleaf);
         rs.rPo = make_rsrc(e.p_out + pb, nleaf);
         rs.rM = make_rsrc(e.m + pb, nleaf);
         rs.rV = make_rsrc(e.v + pb, nleaf);
-        hasT = e.target != nullptr;
-        rs.rT = make_rsrc(uniptr(hasT ? e.target + (long long)tt.slot * e.PT + e.w_off[tt.gi] + (long long)tt.y * e.ens
-                                      : e.m + pb), nleaf);
+        rs.hasT = e.target != nullptr;
+        rs.rT = make_rsrc(uniptr(rs.hasT ? e.target + (long long)tt.slot * e.PT + e.w_off[tt.gi] + (long long)tt.y * e.ens
+                                         : e.m + pb), nleaf);
+        return rs;
     };
-    float4 p4[3], m4[3], v4[3], t4[3];
-    auto issue = [&](const Res& rs, bool hasT, int ldc, int i0, int j0, int u, int q) {
-        const int off = ((i0 + u * 8 + ri) * ldc + j0 + cj) * 4;
+    // unit u of a tile (rows 8 u + ri, columns cj .. cj + 3) in slot u % (D + 1): 8 units per
+    // tile, a multiple of D + 1, so a unit's slot is the same in every tile
+    float4 p4[D + 1], m4[D + 1], v4[D + 1], t4[D + 1];
+    auto issue = [&](const Res& rs, const WsTile& tt, int u, int q) {
+        const int off = ((tt.i0 + u * 8 + ri) * rs.ldc + tt.j0 + cj) * 4;
         p4[q] = bload4_aux(rs.rP, off, 0);
         m4[q] = bload4_aux(rs.rM, off, 1);
         v4[q] = bload4_aux(rs.rV, off, 1);
-        t4[q] = hasT ? bload4_aux(rs.rT, off, 1) : float4{0.f, 0.f, 0.f, 0.f};
+        t4[q] = rs.hasT ? bload4_aux(rs.rT, off, 1) : float4{0.f, 0.f, 0.f, 0.f};
     };
-    WsTile t = ws_tile(ga, tile_id(0));
-    Res rs;
-    bool hasT;
-    int gM, ldc;
-    tile_res(t, rs, hasT, gM, ldc);
-    ws_barrier();  // G's prologue barrier
-    for (int it = 0; it <= ntl; ++it) {
-        if (it >= 1) {
-            // tile it - 1 (its gradient is in Gt; units 0 and 1 were issued at the last boundary)
-            const float tc = (float)(e.count[t.slot] + 1);
+    static_assert(NU % (D + 1) == 0, "unit slots must repeat per tile");
+    // ta: the tile of the next Adam pass; tw: the tile whose W^T is written next period
+    WsTile ta = ws_tile(ga, tile_id(0));
+    Res ra = tile_res(ta);
+#pragma unroll
+    for (int u = 0; u < D; ++u) issue(ra, ta, u, u);
+    WsTile tw = ta;
+    int gMw = ra.gM;
+    for (int it = 0; it < ntl + 2; ++it) {
+        // (1) tile it - 2: its W^T from gradient buffer it & 1 (new p, written by its Adam pass
+        // last period) and its grad stats from red[(it - 2) & 1]
+        if (it >= 2) {
+            float* const Gw = smem + (it & 1) * BM * PT;
+            if (otid == 0) {
+                const float* rr = red + ((it - 2) & 1) * 12;
+                float* st = e.stats + ((long long)tw.slot * e.n_total_chunks + e.stat_base[tw.gi] + tw.y * tw.per + tw.tile) * 3;
+                st[0] = fmaxf(fmaxf(rr[0], rr[1]), fmaxf(rr[2], rr[3]));
+                st[1] = fminf(fminf(rr[4], rr[5]), fminf(rr[6], rr[7]));
+                st[2] = rr[8] + rr[9] + rr[10] + rr[11];
+            }
+            if (e.wt_off[tw.gi] >= 0) {
+                float* __restrict__ WT = e.wt_out + (long long)tw.slot * e.PTT + e.wt_off[tw.gi] + (long long)tw.y * e.wt_sy;
+                constexpr int TPC = BM / 4;
+                for (int q = opq(otid); q < BM * BN / 4; q += 256) {
+                    const int jj = q / TPC, ii = (q % TPC) * 4;
+                    const float* g4 = Gw + ii * PT + jj;
+                    *reinterpret_cast<float4*>(WT + (long long)(tw.j0 + jj) * gMw + tw.i0 + ii) =
+                        float4{g4[0], g4[PT], g4[2 * PT], g4[3 * PT]};
+                }
+            }
+        }
+        // (2) tile it - 1: optax.adam / EMA / stats from gradient buffer (it - 1) & 1, the new p
+        // back into it; the loads of the next D units are in flight throughout (the last D of
+        // them belong to tile it)
+#if defined(FQ_WS_SKIP) && FQ_WS_SKIP == 2
+        if (false) {
+#else
+        if (it >= 1 && it <= ntl) {
+#endif
+            float* const Ga = smem + ((it - 1) & 1) * BM * PT;
+            const bool more = it < ntl;
+            const WsTile tn = more ? ws_tile(ga, tile_id(it)) : ta;
+            const Res rn = more ? tile_res(tn) : ra;
+            const float tc = (float)(e.count[ta.slot] + 1);
             const float bc1 = 1.0f - powf(0.9f, tc), bc2 = 1.0f - powf(0.999f, tc);
             const float rbc1 = 1.0f / bc1, rbc2 = 1.0f / bc2;
-            const int rows = min(BM, gM - t.i0);
+            const int rows = min(BM, ra.gM - ta.i0);
             float mx = -INFINITY, mn = INFINITY, ss = 0.f;
 #pragma unroll
-            for (int u = 0; u < WS_NU; ++u) {
-                // unit u: row 8 u + ri, columns cj .. cj + 3 (adam_epilogue's per-thread order)
-                const int q = u % 3;
-                if (u + 2 < WS_NU) issue(rs, hasT, ldc, t.i0, t.j0, u + 2, (u + 2) % 3);
+            for (int u = 0; u < NU; ++u) {
+                const int q = u % (D + 1);
                 const int i = u * 8 + ri;
-                const int off = ((t.i0 + i) * ldc + t.j0 + cj) * 4;
+                const int off = ((ta.i0 + i) * ra.ldc + ta.j0 + cj) * 4;
                 const bool live = i < rows;
-                float* gs = Gt + i * PT + cj;
+                float* gs = Ga + i * PT + cj;
                 float pp[4] = {p4[q].x, p4[q].y, p4[q].z, p4[q].w};
                 float mm[4] = {m4[q].x, m4[q].y, m4[q].z, m4[q].w};
                 float vv[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
@@ -978,62 +1003,33 @@ __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga
                     mn = live ? fminf(mn, gr) : mn;
                     ss = live ? fmaf(gr, gr, ss) : ss;
                 }
-                bstore4_aux(rs.rPo, float4{pp[0], pp[1], pp[2], pp[3]}, off, 0);
-                bstore4_aux(rs.rM, float4{mm[0], mm[1], mm[2], mm[3]}, off, 1);
-                bstore4_aux(rs.rV, float4{vv[0], vv[1], vv[2], vv[3]}, off, 1);
-                if (hasT) bstore4_aux(rs.rT, float4{tt[0], tt[1], tt[2], tt[3]}, off, 1);
-                // the stats chains are folded in this unit (the compiler otherwise sinks them
-                // past the barriers and keeps every unit's gradient values live: 72 spilled VGPRs)
+                // the slot is free: the unit D ahead (this tile's, or the next one's)
+                if (u + D < NU) issue(ra, ta, u + D, (u + D) % (D + 1));
+                else if (more) issue(rn, tn, u + D - NU, (u + D) % (D + 1));
+                bstore4_aux(ra.rPo, float4{pp[0], pp[1], pp[2], pp[3]}, off, 0);
+                bstore4_aux(ra.rM, float4{mm[0], mm[1], mm[2], mm[3]}, off, 1);
+                bstore4_aux(ra.rV, float4{vv[0], vv[1], vv[2], vv[3]}, off, 1);
+                if (ra.hasT) bstore4_aux(ra.rT, float4{tt[0], tt[1], tt[2], tt[3]}, off, 1);
+                // fold the stats chains in this unit (the compiler otherwise keeps every unit's
+                // gradient values live to the end)
                 asm volatile("" : "+v"(mx), "+v"(mn), "+v"(ss));
-                if (u + 1 == WS_NU) {
-                    // the tile's grad stats: per wave, then the 4 O waves through red[] (read
-                    // after the next barrier)
-                    mx = wave_max(mx);
-                    mn = wave_min(mn);
-                    ss = wave_sum(ss);
-                    if ((otid & 63) == 0) {
-                        red[ow] = mx;
-                        red[4 + ow] = mn;
-                        red[8 + ow] = ss;
-                    }
-                }
-                ws_barrier();
             }
-            if (otid == 0) {
-                float* st = e.stats + ((long long)t.slot * e.n_total_chunks + e.stat_base[t.gi] + t.y * t.per + t.tile) * 3;
-                st[0] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-                st[1] = fminf(fminf(red[4], red[5]), fminf(red[6], red[7]));
-                st[2] = red[8] + red[9] + red[10] + red[11];
+            mx = wave_max(mx);
+            mn = wave_min(mn);
+            ss = wave_sum(ss);
+            if ((otid & 63) == 0) {
+                float* rr = red + ((it - 1) & 1) * 12;
+                rr[ow] = mx;
+                rr[4 + ow] = mn;
+                rr[8 + ow] = ss;
             }
-            // W^T[j][i0 .. i0 + BM) as float4 runs along i (hidden layers: M = H, full tiles)
-            const bool wt = e.wt_off[t.gi] >= 0;
-            float* __restrict__ WT = wt ? e.wt_out + (long long)t.slot * e.PTT + e.wt_off[t.gi] + (long long)t.y * e.wt_sy
-                                        : nullptr;
-            for (int u = 0; u < WS_NU; ++u) {
-                if (wt) {
-                    // (the lane index through an opaque copy: per-unit addresses are computed here,
-                    // not hoisted to the kernel top and spilled)
-                    constexpr int TPC = BM / 4;
-                    const int qq = opq(otid) + 256 * u;
-                    const int jj = qq / TPC, ii = (qq % TPC) * 4;
-                    const float* src = Gt + ii * PT + jj;
-                    *reinterpret_cast<float4*>(WT + (long long)(t.j0 + jj) * gM + t.i0 + ii) =
-                        float4{src[0], src[PT], src[2 * PT], src[3 * PT]};
-                }
-                ws_barrier();
-            }
-        } else {
-            for (int u = 0; u < 2 * WS_NU; ++u) ws_barrier();
+            tw = ta;
+            gMw = ra.gM;
+            ta = tn;
+            ra = rn;
         }
-        for (int kt = 2 * WS_NU; kt < nph; ++kt) ws_barrier();
-        // period boundary: the next tile's first units go in flight while G writes its gradient tile
-        if (it < ntl) {
-            t = ws_tile(ga, tile_id(it));
-            tile_res(t, rs, hasT, gM, ldc);
-            issue(rs, hasT, ldc, t.i0, t.j0, 0, 0);
-            issue(rs, hasT, ldc, t.i0, t.j0, 1, 1);
-        }
-        ws_barrier();
+        ws_barrier();  // A
+        ws_barrier();  // B
     }
 }
 
@@ -1052,6 +1048,11 @@ void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, c
     }
     ga.first[ng] = tot;
     ga.ng = ng;
+    bool ws_ok = true;  // the wave-specialised launch: one K for all problems, K % 32 == 0
+    for (int i = 0; i < ng; ++i) ws_ok = ws_ok && gs[i].K == gs[0].K && gs[i].K % 32 == 0;
+    if (adam && tile == 14 && !ws_ok) {  // its tiles, i.e. its stats chunks, are tile 10's
+        tile = 10;
+    }
     if (adam && tile == 14) {
         // wave-specialised persistent launch: 2 blocks per CU over the tiles, then the
         // small-leaf blocks
@@ -1389,43 +1390,6 @@ DEV void ef_tail(f32x4 (&acc)[4], float4 a, const float* xs, int lk, int li) {
     acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b, acc[1], 0, 0, 0);
     acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b, acc[2], 0, 0, 0);
     acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b, acc[3], 0, 0, 0);
-}
-
-// The dX product dh^T = du^T W_l^T of the streamed backward reading W_l [k][j] itself (no W_l^T
-// copy).  The output layout is ef_kloop's (tile c, A row li = feature 64w + 4li + c); the
-// reduction index of k-step s = 4t + q is j = 16t + 4lk + q, so a lane's float4
-// W_l[64w + 4li + c][16t + 4lk .. +3] feeds tile c's MFMAs of the 4 k-steps of group t (a row
-// is read in 64-B runs: 4 lanes per row, 16 rows per load instruction).  ring[g][c] holds
-// group t0 + g of tile c; NG groups (4 NG k-steps) in flight, refilled across the layer
-// boundary from the next product's W (w_next) as ef_kloop's ring does.
-template <int NG>
-DEV void bw_kloop(f32x4 (&acc)[4], float4 (&ring)[NG][4], rsrc_t rW, const float* xs, int NTG, int w_cur,
-                  int w_next, int lo, int lk, int li) {
-    constexpr int NC = EF_NC, H = EF_H;
-    int t0 = 0;
-    do {
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            const int t = t0 + g;
-            float b[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) b[q] = xs[(16 * t + 4 * lk + q) * NC + li];
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float av[4] = {ring[g][0][q], ring[g][1][q], ring[g][2][q], ring[g][3][q]};
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c], b[q], acc[c], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            // refill: group t + NG of this product, or group t + NG - NTG of the next one
-            const int base = t + NG < NTG ? w_cur + 16 * (t + NG) : w_next + 16 * (t + NG - NTG);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) ring[g][c] = bload4(rW, base + lo + c * H);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        t0 += NG;
-    } while (t0 < NTG);
 }
 
 bool euler_flow_supported(int H, int L, int D, int A, int B) {
@@ -2241,12 +2205,9 @@ bool stream_bwd_supported(int H, int L, int nout, int M, int Mg) {
            Mg % EF_NC == 0 && Mg <= M;
 }
 
-template <bool LN, bool WD = false>
+template <bool LN>
 __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(const StreamBwdArgs g) {
     constexpr int H = EF_H, NC = EF_NC, NT = EF_NW * 64, PF = sb_pf<LN>();
-    // WD (actor nets): the dX products read W_l directly (bw_kloop), 2 groups of 4 k-steps in flight
-    static_assert(!(WD && LN), "W-direct backward: actor (no LayerNorm) variant only");
-    constexpr int NG = 2;
     __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];  // du_l [H][NC] (+ look-ahead slack)
     __shared__ __attribute__((aligned(16))) float scr[H * NC];         // head kernel W_L [H][nout]; then LN-grad products
     __shared__ float colred[2][EF_NW][NC];                            // LN column-stat partials per wave
@@ -2317,23 +2278,11 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
     // waited for the ring refills of the next product, every layer)
     const int lo = lk * H + 64 * w + 4 * li;
     float4 ring[PF];
-    // W-direct: lane offset of W_l[64w + 4li][4lk] (tile c: + c H, group t: + 16 t)
-    const int lo_w = (64 * w + 4 * li) * H + 4 * lk;
-    const rsrc_t rWd = make_rsrc(P, g.ens);
-    float4 ringw[WD ? NG : 1][4];
     auto load_first = [&]() {
         load_epi(L - 1, tid, li, lk);
-        if constexpr (WD) {
-            const int wf = L > 1 ? (int)g.w_off[L - 1] : 0;
+        const int wf = L > 1 ? (int)g.wt_off[L - 1] : 0;
 #pragma unroll
-            for (int gg = 0; gg < NG; ++gg)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) ringw[gg][c] = bload4(rWd, wf + 16 * gg + lo_w + c * H);
-        } else {
-            const int wf = L > 1 ? (int)g.wt_off[L - 1] : 0;
-#pragma unroll
-            for (int p = 0; p < PF; ++p) ring[p] = bload4(rT, wf + 4 * p * H + lo);
-        }
+        for (int p = 0; p < PF; ++p) ring[p] = bload4(rT, wf + 4 * p * H + lo);
     };
     // lane layout (as ef_kloop's accumulators): column li, features f = 64w + 16lk + 4r + c
     // last hidden layer: dh = W_L dout (nout <= 8, VALU)
@@ -2556,14 +2505,8 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         f32x4 acc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (WD) {
-            const int wn = (int)g.w_off[l >= 2 ? l - 1 : l];  // next product's W (l-1 >= 1), else a harmless re-load
-            bw_kloop<NG>(acc, ringw, rWd, slab, H / 16, (int)g.w_off[l], wn, (64 * w + 4 * li_l) * H + 4 * lk_l, lk_l,
-                         li_l);
-        } else {
-            const int wn = (int)g.wt_off[l >= 2 ? l - 1 : l];  // next product's W^T (l-1 >= 1), else a harmless re-load
-            ef_kloop<PF>(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lk_l * H + 64 * w + 4 * li_l, lk_l, li_l);
-        }
+        const int wn = (int)g.wt_off[l >= 2 ? l - 1 : l];  // next product's W^T (l-1 >= 1), else a harmless re-load
+        ef_kloop<PF>(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lk_l * H + 64 * w + 4 * li_l, lk_l, li_l);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -2580,7 +2523,6 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
 void launch_stream_bwd(bool ln, const StreamBwdArgs& a, hipStream_t s) {
     const dim3 grid((a.M / EF_NC) * a.ny * a.nz), block(EF_NW * 64);
     if (ln) hipLaunchKernelGGL((stream_bwd_kernel<true>), grid, block, 0, s, a);
-    else if (a.wdirect) hipLaunchKernelGGL((stream_bwd_kernel<false, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((stream_bwd_kernel<false>), grid, block, 0, s, a);
 }
 

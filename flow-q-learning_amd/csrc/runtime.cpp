@@ -78,7 +78,6 @@ struct EngineOptions {
     int dw_tile_critic = 10, dw_tile_actor = 10;  // grouped dW tile ids (launch_gemm_group_dw)
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
     int dw_stagger = 0;    // fused dW + optimiser: first-wave start offsets (AdamEpi::stagger)
-    int bwd_wdirect = 0;   // actor backwards read W_l directly: no W^T copies of the actor nets
     int dw_persist = 0;    // tile 14: persistent blocks of the wave-specialised launch (0: 2 per CU)
 };
 EngineOptions g_engine_opts;
@@ -97,7 +96,6 @@ const EngineOptionRef kEngineOptions[] = {
     {"dw_tile_actor", &EngineOptions::dw_tile_actor, 0, 14},
     {"adam_nt", &EngineOptions::adam_nt, 0, 3},
     {"dw_stagger", &EngineOptions::dw_stagger, 0, 256},
-    {"bwd_wdirect", &EngineOptions::bwd_wdirect, 0, 1},
     {"dw_persist", &EngineOptions::dw_persist, 0, 1 << 20},
 };
 
@@ -661,10 +659,6 @@ AdamArgs adam_args(const Ctx& c, int ni);
 // ld `ld_d`; M columns are back-propagated, the first Mg feed the grads.
 int skip_mask();
 
-// net ni's streamed backward reads W_l directly (engine option bwd_wdirect, actor nets): no
-// W^T copy of it is written
-bool wt_direct(const fqlpop* h, int ni) { return ni != 0 && h->opt.bwd_wdirect != 0 && !h->bc.ln; }
-
 void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, int ld_o, TRef X0, int ld,
                     long long coff, int M, int Mg, const std::vector<float*>& U, const std::vector<float*>& G,
                     long long act_sy, const std::vector<float*>* MU, const std::vector<float*>* RS, long long st_sy,
@@ -702,7 +696,6 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
     a.part = part; a.NP = stream_bwd_np(N.L, N.H, N.out_dim, N.ln);
     a.L = N.L; a.M = M; a.Mg = Mg; a.nout = N.out_dim;
     a.ny = N.E; a.nz = c.nz; a.slots = h->slots;
-    a.wdirect = wt_direct(h, ni) ? 1 : 0;
     if (ig) {
         // the critic's dQ/da, computed by the backward's layer-0 epilogue (per-ensemble partials)
         ARGCHK(ig->off == Mg && ig->M == M - Mg, "input-grad columns must follow the grad columns");
@@ -762,7 +755,7 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         for (int gi = 0; gi < (int)gs.size(); ++gi) {
             const int l = N.L - 1 - gi;
             ae.w_off[gi] = N.off + N.W[l];
-            ae.wt_off[gi] = l >= 1 && !wt_direct(h, ni) ? h->wt_net_off[ni] + (long long)(l - 1) * N.H * N.H : -1;
+            ae.wt_off[gi] = l >= 1 ? h->wt_net_off[ni] + (long long)(l - 1) * N.H * N.H : -1;
             ae.stat_base[gi] = h->w_stat_base[ni][l];
         }
         ae.stats = h->stats; ae.n_total_chunks = h->n_chunks_total;

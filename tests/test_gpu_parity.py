@@ -427,11 +427,3 @@ def test_device_init_properties():
         assert pop.get_count(i) == 0
         assert not np.any(pop.get_flat(i, STATE_ADAM_M)) and not np.any(pop.get_flat(i, STATE_ADAM_V))
     pop.close()
-
-
-def test_update_parity_actor_backward_reading_w_directly():
-    """Engine option bwd_wdirect: the actor nets' streamed backward reads W_l itself (its
-    reduction order over j differs from the W^T path's, so the check is parity with the
-    oracle, not bit-identity), and no W^T copy of the actor nets is written."""
-    with engine_options(bwd_wdirect=1):
-        _run_parity(512, 256, [10.0, 100.0], n_steps=2)
