@@ -730,21 +730,30 @@ __global__ __launch_bounds__(256, 4) void gemm_group_kernel_o4(const GemmGroupAr
 // The same work as gemm_group_kernel_o4<64, 128, true, true, EPI_ADAM, 16> (tile id 14),
 // bit-identical, in a persistent launch whose blocks split their 8 waves into two groups
 // that run concurrently:
-//   G (waves 0-3): the dW product of tile n, operand fragments loaded from L2 straight into
-//                  registers (no LDS staging, so no barrier inside the k-loop), the same MFMA
-//                  sequence as gemm_body's KB layout;
-//   O (waves 4-7): optax.adam / the target EMA / grad stats of tile n-1 and the W^T copy of
-//                  tile n-2, from gradient tiles G left in LDS (two buffers), with the p / m /
-//                  v / target loads of the next WS_D units always in flight (across tiles).
-// One tile period ends in two block barriers: A (both groups are done with the period's
-// LDS), then G writes its accumulators into gradient buffer n & 1, then B (published).  In the
-// one-tile-per-block launch every co-resident block ran its k-loop, then its HBM-bound
-// optimiser pass, at the same time as the others (they start together), so the two phases
-// hardly overlapped.
+//   G (waves 0-3): the dW product of tile n, gemm_body's k-loop (operand slices staged through
+//                  LDS in the KB layout, double-buffered, the same MFMA sequence);
+//   O (waves 4-7): optax.adam / the target EMA / grad stats and the W^T copy of tile n - 1
+//                  from the gradient tile G left in LDS, with the p / m / v / target loads of
+//                  the next WS_D units always in flight (across tiles).
+// Inside a tile period each group synchronises only its own 4 waves (ws_group_sync: an LDS
+// arrival counter, so a G k-slice never waits for the optimiser and vice versa); the period
+// ends in two block barriers: A (O is done with the gradient tile), G writes its
+// accumulators into it, B (published).  In the one-tile-per-block launch every co-resident
+// block ran its k-loop, then its HBM-bound optimiser pass, at the same time as the others
+// (they start together), so the two phases hardly overlapped.
 constexpr int WS_BM = 64, WS_BN = 128, WS_BK = 16, WS_PT = WS_BN + 1, WS_NU = 8, WS_D = 3;
-constexpr int WS_SMEM = 2 * WS_BM * WS_PT + 32;
+constexpr int WS_RP = rc_pitch<WS_BK, true>();
+constexpr int WS_STAGE = (WS_BM + WS_BN) * WS_RP;  // one A + B slice
+constexpr int WS_SMEM = WS_BM * WS_PT + 2 * WS_STAGE + 16;
 
 DEV void ws_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// barrier of one 4-wave group: each wave's LDS writes complete, then it counts itself in
+// and waits for the group's 4 arrivals (*ctr counts up by 4 per sync; target = 4 x syncs)
+DEV void ws_group_sync(unsigned* ctr, unsigned target) {
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+}
 
 // block-uniform description of logical tile lt of a grouped launch
 struct WsTile {
@@ -772,7 +781,7 @@ DEV WsTile ws_tile(const GemmGroupArgs& ga, int lt) {
 
 __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga) {
     __shared__ __attribute__((aligned(16))) float smem[WS_SMEM];
-    constexpr int BM = WS_BM, BN = WS_BN, BK = WS_BK, PT = WS_PT, NU = WS_NU, D = WS_D;
+    constexpr int BM = WS_BM, BN = WS_BN, BK = WS_BK, PT = WS_PT, RP = WS_RP, NU = WS_NU, D = WS_D;
     const int nper = ga.adam.persist;  // persistent blocks (a multiple of 8)
     if ((int)blockIdx.x >= nper) {
         const int sb = blockIdx.x - nper, nch = ga.adam.small.n_chunks;
@@ -789,18 +798,24 @@ __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga
     auto tile_id = [&](int n) { return start + jb + n * nbx; };
     const int gK = uni(ga.g[0].K);  // one net: every problem has K = Mg
     const int nk = gK / BK;
-    float* const red = smem + 2 * BM * PT;  // [2][12]: O-wave stats partials of the last two tiles
+    float* const Gt = smem;                            // the gradient tile [BM][PT]
+    float* const stage = smem + BM * PT;               // G: [2][A BM x RP | B BN x RP]
+    float* const red = stage + 2 * WS_STAGE;           // O: [12] wave stats partials
+    unsigned* const ctr = reinterpret_cast<unsigned*>(red + 12);  // [2] group arrival counters
     const AdamEpi& e = ga.adam;
     const int wave = threadIdx.x >> 6;
+    if (threadIdx.x < 2) ctr[threadIdx.x] = 0u;
+    ws_barrier();
 
     if (wave < 4) {
         // ------------------------------------------------------------ G: the dW products
-        const int lane = threadIdx.x & 63;
+        const int tid = threadIdx.x, lane = tid & 63;
         const int wi = (wave >> 1) * (BM / 2), wj = (wave & 1) * (BN / 2);
         const int l32 = lane & 31, lh = lane >> 5;
+        unsigned syncs = 0;
         struct Src {
             rsrc_t rA, rB;
-            int lda, ldb;
+            int lda, ldb, i0, j0;
         };
         auto src = [&](const WsTile& tt) {
             const GemmArgs& g = ga.g[tt.gi];
@@ -810,82 +825,98 @@ __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga
             r.ldb = uni(g.ldb);
             r.rA = make_rsrc(uniptr(at(g.A, tt.slot, tt.y)), (long long)(gM - 1) * r.lda + gK);
             r.rB = make_rsrc(uniptr(at(g.B, tt.slot, tt.y)), (long long)(gN - 1) * r.ldb + gK);
+            r.i0 = tt.i0;
+            r.j0 = tt.j0;
             return r;
         };
-        // slice kt's fragments of this lane: A[i0 + wi + l32][16 kt + 8 lh .. +7] (the KB layout's
-        // k-blocked order: MFMA kk of lane half lh takes k = 8 lh + kk), B the same for columns
-        // j0 + wj + l32 and j0 + wj + 32 + l32 (rows past M read 0: buffer range)
-        auto load = [&](float4 (&f)[6], const Src& r, const WsTile& tt, int kt) {
-            const int k = kt * BK + 8 * lh;
-            const int oa = (tt.i0 + wi + l32) * r.lda + k;
-            const int ob0 = (tt.j0 + wj + l32) * r.ldb + k, ob1 = ob0 + 32 * r.ldb;
-            f[0] = bload4(r.rA, oa);
-            f[1] = bload4(r.rA, oa + 4);
-            f[2] = bload4(r.rB, ob0);
-            f[3] = bload4(r.rB, ob0 + 4);
-            f[4] = bload4(r.rB, ob1);
-            f[5] = bload4(r.rB, ob1 + 4);
+        // slice staging, as gemm_body: 1 A + 2 B float4 per thread, KB layout (pitch RP); two
+        // register sets, set s & 1 holding slice s (slices numbered on across tiles), so a
+        // slice's loads have two k-slices of MFMAs to land in
+        float4 ra[2], rb[2][2];
+        auto load = [&](int set, const Src& r, int k0) {
+            ra[set] = stage_load<BM, BK, true>(r.rA, r.lda, 0, r.i0, k0);
+            rb[set][0] = stage_load<BN, BK, true>(r.rB, r.ldb, 0, r.j0, k0);
+            rb[set][1] = stage_load<BN, BK, true>(r.rB, r.ldb, 1, r.j0, k0);
         };
-        // the MFMAs of one slice, in gemm_body's KB order (k = 8 lh + kk, column halves b = 0, 1)
-        auto slice = [&](f32x16 (&acc)[2], const float4 (&f)[6]) {
-            const float av[8] = {f[0].x, f[0].y, f[0].z, f[0].w, f[1].x, f[1].y, f[1].z, f[1].w};
-            const float bv0[8] = {f[2].x, f[2].y, f[2].z, f[2].w, f[3].x, f[3].y, f[3].z, f[3].w};
-            const float bv1[8] = {f[4].x, f[4].y, f[4].z, f[4].w, f[5].x, f[5].y, f[5].z, f[5].w};
+        auto store = [&](int set, int buf) {
+            float* S = stage + buf * WS_STAGE;
+            stage_store<BM, BK, true, RP>(S, 0, ra[set]);
+            stage_store<BN, BK, true, RP>(S + BM * RP, 0, rb[set][0]);
+            stage_store<BN, BK, true, RP>(S + BM * RP, 1, rb[set][1]);
+        };
+        // one k-slice: loads of slice kt + 2 (or the next tile's) into set kt & 1, MFMAs
+        // on LDS buffer kt & 1, then slice kt + 1 from set (kt + 1) & 1 into the other buffer
+        auto step = [&](f32x16 (&acc)[2], int kt, int set, const Src& sr, const Src& srn) {
+            {  // selected, not branched: loads on both sides of a branch get
+               // over-conservative vmcnt waits after the join
+                const bool in = kt + 2 < nk;
+                Src sx;
+                sx.rA = in ? sr.rA : srn.rA;
+                sx.rB = in ? sr.rB : srn.rB;
+                sx.lda = in ? sr.lda : srn.lda;
+                sx.ldb = in ? sr.ldb : srn.ldb;
+                sx.i0 = in ? sr.i0 : srn.i0;
+                sx.j0 = in ? sr.j0 : srn.j0;
+                load(set, sx, (in ? kt + 2 : kt + 2 - nk) * BK);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            const float* S = stage + set * WS_STAGE;
+            float av[8], bv[8][2];
+            {
+                const float* r = S + (wi + l32) * RP + 8 * lh;
+                const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
+                av[0] = x0.x; av[1] = x0.y; av[2] = x0.z; av[3] = x0.w;
+                av[4] = x1.x; av[5] = x1.y; av[6] = x1.z; av[7] = x1.w;
+            }
 #pragma unroll
-            for (int kk = 0; kk < 8; ++kk) {
-                acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv0[kk], acc[0], 0, 0, 0);
-                acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv1[kk], acc[1], 0, 0, 0);
+            for (int b = 0; b < 2; ++b) {
+                const float* r = S + BM * RP + (wj + b * 32 + l32) * RP + 8 * lh;
+                const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
+                bv[0][b] = x0.x; bv[1][b] = x0.y; bv[2][b] = x0.z; bv[3][b] = x0.w;
+                bv[4][b] = x1.x; bv[5][b] = x1.y; bv[6][b] = x1.z; bv[7][b] = x1.w;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk][b], acc[b], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (kt + 1 < nk) {
+                store(set ^ 1, set ^ 1);
+                ws_group_sync(ctr, syncs += 4);
             }
         };
-        WsTile t = ws_tile(ga, tile_id(0));
-        Src sr = src(t);
-        float4 cur[6], nxt[6];
-        load(cur, sr, t, 0);
-        for (int it = 0; it < ntl + 2; ++it) {  // + 2 periods: O's last Adam and W^T passes
+        {
+            const WsTile t0 = ws_tile(ga, tile_id(0));
+            const Src s0 = src(t0);
+            load(0, s0, 0);
+            load(1, s0, BK);
+        }
+        Src sr = src(ws_tile(ga, tile_id(0)));
+        for (int it = 0; it <= ntl; ++it) {  // + 1 period: O's pass over the last tile
             f32x16 acc[2];
             if (it < ntl) {
                 const bool more = it + 1 < ntl;
-                const WsTile tn = more ? ws_tile(ga, tile_id(it + 1)) : t;
-                const Src srn = more ? src(tn) : sr;
+                const Src srn = more ? src(ws_tile(ga, tile_id(it + 1))) : sr;
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-                // two slices per trip, the fragment registers ping-ponged (a register copy of
-                // a prefetch would wait for it); nk is even (the launch checks K % 32 == 0)
+                store(0, 0);  // slice 0 (buffer 0 was last read two slices ago, before a sync)
+                ws_group_sync(ctr, syncs += 4);
 #if defined(FQ_WS_SKIP) && FQ_WS_SKIP == 1
                 for (int kt = 0; kt < 0; kt += 2) {
 #else
                 for (int kt = 0; kt < nk; kt += 2) {
 #endif
-                    load(nxt, sr, t, kt + 1);
-                    __builtin_amdgcn_sched_barrier(0);
-                    slice(acc, cur);
-                    __builtin_amdgcn_sched_barrier(0);
-                    // the slice after, or after the last one the next tile's first
-                    {  // selected, not branched: loads on both sides of a branch get
-                       // over-conservative vmcnt waits in the MFMAs after the join
-                        const bool in = kt + 2 < nk;
-                        Src sx;
-                        sx.rA = in ? sr.rA : srn.rA;
-                        sx.rB = in ? sr.rB : srn.rB;
-                        sx.lda = in ? sr.lda : srn.lda;
-                        sx.ldb = in ? sr.ldb : srn.ldb;
-                        WsTile tx = tn;
-                        tx.i0 = in ? t.i0 : tn.i0;
-                        tx.j0 = in ? t.j0 : tn.j0;
-                        load(cur, sx, tx, in ? kt + 2 : 0);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                    slice(acc, nxt);
-                    __builtin_amdgcn_sched_barrier(0);
+                    step(acc, kt, 0, sr, srn);
+                    step(acc, kt + 1, 1, sr, srn);
                 }
-                t = tn;
                 sr = srn;
             }
-            ws_barrier();  // A: O is done with gradient buffer it & 1 (its W^T pass of tile it - 2)
+            ws_barrier();  // A: O is done with the gradient tile (tile it - 1)
             if (it < ntl) {
-                float* const Gt = smem + (it & 1) * BM * PT;
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -902,6 +933,7 @@ __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga
     constexpr int TPR = BN / 4;  // 32 threads per row, 8 rows per unit
     const int cj = (otid % TPR) * 4, ri = otid / TPR;
     const float lr = e.lr, tau = e.tau;
+    unsigned syncs = 0;
     struct Res {
         rsrc_t rP, rPo, rM, rV, rT;
         int gM, ldc;
@@ -934,100 +966,86 @@ __global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga
         t4[q] = rs.hasT ? bload4_aux(rs.rT, off, 1) : float4{0.f, 0.f, 0.f, 0.f};
     };
     static_assert(NU % (D + 1) == 0, "unit slots must repeat per tile");
-    // ta: the tile of the next Adam pass; tw: the tile whose W^T is written next period
-    WsTile ta = ws_tile(ga, tile_id(0));
+    WsTile ta = ws_tile(ga, tile_id(0));  // the tile of the next pass
     Res ra = tile_res(ta);
 #pragma unroll
     for (int u = 0; u < D; ++u) issue(ra, ta, u, u);
-    WsTile tw = ta;
-    int gMw = ra.gM;
-    for (int it = 0; it < ntl + 2; ++it) {
-        // (1) tile it - 2: its W^T from gradient buffer it & 1 (new p, written by its Adam pass
-        // last period) and its grad stats from red[(it - 2) & 1]
-        if (it >= 2) {
-            float* const Gw = smem + (it & 1) * BM * PT;
-            if (otid == 0) {
-                const float* rr = red + ((it - 2) & 1) * 12;
-                float* st = e.stats + ((long long)tw.slot * e.n_total_chunks + e.stat_base[tw.gi] + tw.y * tw.per + tw.tile) * 3;
-                st[0] = fmaxf(fmaxf(rr[0], rr[1]), fmaxf(rr[2], rr[3]));
-                st[1] = fminf(fminf(rr[4], rr[5]), fminf(rr[6], rr[7]));
-                st[2] = rr[8] + rr[9] + rr[10] + rr[11];
+    ws_barrier();  // A (period 0: G's first k-loop)
+    ws_barrier();  // B
+    for (int it = 1; it <= ntl; ++it) {
+        // tile it - 1: optax.adam / EMA / stats from the gradient tile, the new p back into it;
+        // the loads of the next D units are in flight throughout (the last D of them belong
+        // to tile it)
+#if !(defined(FQ_WS_SKIP) && FQ_WS_SKIP == 2)
+        const bool more = it < ntl;
+        const WsTile tn = more ? ws_tile(ga, tile_id(it)) : ta;
+        const Res rn = more ? tile_res(tn) : ra;
+        const float tc = (float)(e.count[ta.slot] + 1);
+        const float bc1 = 1.0f - powf(0.9f, tc), bc2 = 1.0f - powf(0.999f, tc);
+        const float rbc1 = 1.0f / bc1, rbc2 = 1.0f / bc2;
+        const int rows = min(BM, ra.gM - ta.i0);
+        float mx = -INFINITY, mn = INFINITY, ss = 0.f;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int q = u % (D + 1);
+            const int i = u * 8 + ri;
+            const int off = ((ta.i0 + i) * ra.ldc + ta.j0 + cj) * 4;
+            const bool live = i < rows;
+            float* gs = Gt + i * PT + cj;
+            float pp[4] = {p4[q].x, p4[q].y, p4[q].z, p4[q].w};
+            float mm[4] = {m4[q].x, m4[q].y, m4[q].z, m4[q].w};
+            float vv[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
+            float tt[4] = {t4[q].x, t4[q].y, t4[q].z, t4[q].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float gr = gs[c];
+                adam_moments(gr, mm[c], vv[c]);
+                tt[c] = ema_target(pp[c], tt[c], tau);
+                pp[c] = adam_step_fast(pp[c], mm[c], vv[c], rbc1, rbc2, lr);
+                gs[c] = pp[c];
+                mx = live ? fmaxf(mx, gr) : mx;
+                mn = live ? fminf(mn, gr) : mn;
+                ss = live ? fmaf(gr, gr, ss) : ss;
             }
-            if (e.wt_off[tw.gi] >= 0) {
-                float* __restrict__ WT = e.wt_out + (long long)tw.slot * e.PTT + e.wt_off[tw.gi] + (long long)tw.y * e.wt_sy;
-                constexpr int TPC = BM / 4;
-                for (int q = opq(otid); q < BM * BN / 4; q += 256) {
-                    const int jj = q / TPC, ii = (q % TPC) * 4;
-                    const float* g4 = Gw + ii * PT + jj;
-                    *reinterpret_cast<float4*>(WT + (long long)(tw.j0 + jj) * gMw + tw.i0 + ii) =
-                        float4{g4[0], g4[PT], g4[2 * PT], g4[3 * PT]};
-                }
+            // the slot is free: the unit D ahead (this tile's, or the next one's)
+            if (u + D < NU) issue(ra, ta, u + D, (u + D) % (D + 1));
+            else if (more) issue(rn, tn, u + D - NU, (u + D) % (D + 1));
+            bstore4_aux(ra.rPo, float4{pp[0], pp[1], pp[2], pp[3]}, off, 0);
+            bstore4_aux(ra.rM, float4{mm[0], mm[1], mm[2], mm[3]}, off, 1);
+            bstore4_aux(ra.rV, float4{vv[0], vv[1], vv[2], vv[3]}, off, 1);
+            if (ra.hasT) bstore4_aux(ra.rT, float4{tt[0], tt[1], tt[2], tt[3]}, off, 1);
+            // fold the stats chains in this unit (the compiler otherwise keeps every unit's
+            // gradient values live to the end)
+            asm volatile("" : "+v"(mx), "+v"(mn), "+v"(ss));
+        }
+        mx = wave_max(mx);
+        mn = wave_min(mn);
+        ss = wave_sum(ss);
+        if ((otid & 63) == 0) {
+            red[ow] = mx;
+            red[4 + ow] = mn;
+            red[8 + ow] = ss;
+        }
+        ws_group_sync(ctr + 1, syncs += 4);  // the new p of every row, the stats partials
+        if (otid == 0) {
+            float* st = e.stats + ((long long)ta.slot * e.n_total_chunks + e.stat_base[ta.gi] + ta.y * ta.per + ta.tile) * 3;
+            st[0] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+            st[1] = fminf(fminf(red[4], red[5]), fminf(red[6], red[7]));
+            st[2] = red[8] + red[9] + red[10] + red[11];
+        }
+        if (e.wt_off[ta.gi] >= 0) {
+            float* __restrict__ WT = e.wt_out + (long long)ta.slot * e.PTT + e.wt_off[ta.gi] + (long long)ta.y * e.wt_sy;
+            constexpr int TPC = BM / 4;
+            for (int q = opq(otid); q < BM * BN / 4; q += 256) {
+                const int jj = q / TPC, ii = (q % TPC) * 4;
+                const float* g4 = Gt + ii * PT + jj;
+                *reinterpret_cast<float4*>(WT + (long long)(ta.j0 + jj) * ra.gM + ta.i0 + ii) =
+                    float4{g4[0], g4[PT], g4[2 * PT], g4[3 * PT]};
             }
         }
-        // (2) tile it - 1: optax.adam / EMA / stats from gradient buffer (it - 1) & 1, the new p
-        // back into it; the loads of the next D units are in flight throughout (the last D of
-        // them belong to tile it)
-#if defined(FQ_WS_SKIP) && FQ_WS_SKIP == 2
-        if (false) {
-#else
-        if (it >= 1 && it <= ntl) {
+        ta = tn;
+        ra = rn;
 #endif
-            float* const Ga = smem + ((it - 1) & 1) * BM * PT;
-            const bool more = it < ntl;
-            const WsTile tn = more ? ws_tile(ga, tile_id(it)) : ta;
-            const Res rn = more ? tile_res(tn) : ra;
-            const float tc = (float)(e.count[ta.slot] + 1);
-            const float bc1 = 1.0f - powf(0.9f, tc), bc2 = 1.0f - powf(0.999f, tc);
-            const float rbc1 = 1.0f / bc1, rbc2 = 1.0f / bc2;
-            const int rows = min(BM, ra.gM - ta.i0);
-            float mx = -INFINITY, mn = INFINITY, ss = 0.f;
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                const int q = u % (D + 1);
-                const int i = u * 8 + ri;
-                const int off = ((ta.i0 + i) * ra.ldc + ta.j0 + cj) * 4;
-                const bool live = i < rows;
-                float* gs = Ga + i * PT + cj;
-                float pp[4] = {p4[q].x, p4[q].y, p4[q].z, p4[q].w};
-                float mm[4] = {m4[q].x, m4[q].y, m4[q].z, m4[q].w};
-                float vv[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
-                float tt[4] = {t4[q].x, t4[q].y, t4[q].z, t4[q].w};
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float gr = gs[c];
-                    adam_moments(gr, mm[c], vv[c]);
-                    tt[c] = ema_target(pp[c], tt[c], tau);
-                    pp[c] = adam_step_fast(pp[c], mm[c], vv[c], rbc1, rbc2, lr);
-                    gs[c] = pp[c];
-                    mx = live ? fmaxf(mx, gr) : mx;
-                    mn = live ? fminf(mn, gr) : mn;
-                    ss = live ? fmaf(gr, gr, ss) : ss;
-                }
-                // the slot is free: the unit D ahead (this tile's, or the next one's)
-                if (u + D < NU) issue(ra, ta, u + D, (u + D) % (D + 1));
-                else if (more) issue(rn, tn, u + D - NU, (u + D) % (D + 1));
-                bstore4_aux(ra.rPo, float4{pp[0], pp[1], pp[2], pp[3]}, off, 0);
-                bstore4_aux(ra.rM, float4{mm[0], mm[1], mm[2], mm[3]}, off, 1);
-                bstore4_aux(ra.rV, float4{vv[0], vv[1], vv[2], vv[3]}, off, 1);
-                if (ra.hasT) bstore4_aux(ra.rT, float4{tt[0], tt[1], tt[2], tt[3]}, off, 1);
-                // fold the stats chains in this unit (the compiler otherwise keeps every unit's
-                // gradient values live to the end)
-                asm volatile("" : "+v"(mx), "+v"(mn), "+v"(ss));
-            }
-            mx = wave_max(mx);
-            mn = wave_min(mn);
-            ss = wave_sum(ss);
-            if ((otid & 63) == 0) {
-                float* rr = red + ((it - 1) & 1) * 12;
-                rr[ow] = mx;
-                rr[4 + ow] = mn;
-                rr[8 + ow] = ss;
-            }
-            tw = ta;
-            gMw = ra.gM;
-            ta = tn;
-            ra = rn;
-        }
         ws_barrier();  // A
         ws_barrier();  // B
     }
