@@ -236,7 +236,8 @@ def test_train_env_model_driver(tmp_path):
     data = tmp_path / "data"
     data.mkdir()
     np.savez(data / "cube-single-play.npz", observations=ds["observations"], actions=ds["actions"],
-             next_observations=ds["next_observations"], rewards=ds["rewards"])
+             next_observations=ds["next_observations"], rewards=ds["rewards"],
+             masks=(ds["rewards"] != 0).astype(np.float32))  # OGBench singletask: masks = 1 - success
     common = [f"--data_directory={data}", f"--save_directory={tmp_path / 'exp'}", "--val_batches=2"]
     out = tem.main(["--model=termination_predictor", "--steps=150"] + common)
     tp = em.load_flax_msgpack(out / "termination_predictor.pt")["params"]
@@ -290,7 +291,8 @@ def test_multistep_device_sampling_learns_and_driver(tmp_path):
     np.testing.assert_array_equal(runs[0][2], runs[1][2])
     data = tmp_path / "data"
     data.mkdir()
-    np.savez(data / "cube-single-play.npz", **{k: ds[k][:3000] for k in ds})
+    np.savez(data / "cube-single-play.npz", masks=(ds["rewards"][:3000] != 0).astype(np.float32),
+             **{k: ds[k][:3000] for k in ds})
     out = tem.main(["--model=multistep", "--steps=40", "--sequence_length=16", "--termination_weight=0",
                     f"--data_directory={data}", f"--save_directory={tmp_path / 'exp'}", "--val_batches=2"])
     tree = em.load_flax_msgpack(out / "multistep.pt")["params"]
