@@ -445,8 +445,9 @@ def main(argv=None):
             traffic = pmc["traffic_bytes_per_launch"]
 
     result = {
-        "metric": "FQL grad-steps/sec (whole node) over 16-alpha population, cube-single-v0"
-        if args.workload == "cube" else "FQL grad-steps/sec (whole node) over 16-alpha population, antsoccer",
+        # BASELINE.json's metric at the default 16 members per GPU
+        "metric": f"FQL grad-steps/sec (whole node) over {args.members}-α population, "
+                  + ("cube-single-v0" if args.workload == "cube" else "antsoccer"),
         "value": round(value, 2),
         "unit": "member-grad-steps/s",
         "n_gpus": world,
@@ -457,9 +458,10 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (1M transitions of cube-single shape, seeded numpy; random-init weights)",
+        "data": f"synthetic ({args.rows / 1e6:g}M transitions of {args.workload} shape (obs {wl['obs_dim']}, act "
+                f"{wl['action_dim']}), seeded numpy; random-init weights)",
         "config": {
-            "workload": f"{wl['env']} 16-alpha population update(), B={wl['batch_size']}, H=512x4, "
+            "workload": f"{wl['env']} {args.members}-alpha population update(), B={wl['batch_size']}, H=512x4, "
                         f"obs {wl['obs_dim']}, act {wl['action_dim']}, flow_steps 10",
             "members_per_gpu": args.members,
             "global_batch": wl["batch_size"] * args.members * world,

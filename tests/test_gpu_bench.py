@@ -24,6 +24,8 @@ def test_bench_json_contract():
               "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "preheat"):
         assert k in d, k
     assert d["steps"] == 4 and d["warmup"] == 2 and d["n_gpus"] == 1
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        assert d["metric"] == json.load(f)["metric"]  # the north-star metric, verbatim
     assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
     assert d["config"]["info_finite"] is True
     assert abs(d["value"] - 16 * 1000.0 / d["ms_per_step"]) <= 1e-3 * d["value"] + 1.0
