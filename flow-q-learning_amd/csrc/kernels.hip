@@ -2306,13 +2306,15 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
     // last hidden layer: dh = W_L dout (nout <= 8, VALU)
     float dh[4][4];  // [r][c]
     const int w5 = (LN ? 3 : 1) * L * H;  // head kernel grads in the partials
-    load_first();
+    // The head's operands are loaded before the first layer's epilogue inputs and ring: loads
+    // complete in order, so a wait for one issued after those would wait for them too (the
+    // head is on the block's critical path, the ring and epilogue inputs are needed later)
     if (nout == 1) {
         // (the critic: a scalar head) no LDS staging: W_L[f] as float4 runs, this lane's dout,
-        // and G_{L-1} in the accumulator layout, all issued right after the first layer's
-        // epilogue inputs and ring (one memory round trip, no barrier); the head
-        // kernel grads sum_col G_{L-1}[f][col] dout[col] by the DPP reduce-scatter over the
-        // column lanes (lane li ends with feature 64w + 16lk + li = tid)
+        // and G_{L-1} in the accumulator layout, all issued in one batch (one memory round
+        // trip, no barrier); the head kernel grads sum_col G_{L-1}[f][col] dout[col] by the
+        // DPP reduce-scatter over the column lanes (lane li ends with feature 64w + 16lk + li =
+        // tid)
         const rsrc_t rH = make_rsrc(P + g.w_off[L], (long long)H);
         float4 wl[4];
 #pragma unroll
@@ -2325,6 +2327,7 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
 #pragma unroll
             for (int e = 0; e < 16; ++e) gh[e] = bload1(rG, vo, e * g.ld_s * 4);
         }
+        load_first();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float wv[4] = {wl[r].x, wl[r].y, wl[r].z, wl[r].w};
@@ -2337,31 +2340,39 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
             bstore1(rPart, row16_reduce_scatter(gh, li), tid * 4, w5 * 4);
         }
     } else {
-        if (tid < nout * NC) {
+        // dout of the block's columns, row tid (= feature, NT = H) of the head kernel W_L
+        // [H][nout] (nout <= 8), zero-padded to 8 outputs, and this thread's G_{L-1} row (head
+        // kernel grad partials, thread = feature), one batch
+        static_assert(NT == H, "one thread per feature");
+        const bool dl = tid < 8 * NC;
+        float dov = 0.f;
+        if (dl && tid / NC < nout) {
             const int j = tid / NC, col = tid % NC;
-            dos[j][col] = g.dout[(long long)slot * g.dout_ss + (long long)y * g.dout_sy + (long long)j * g.ld_o + c0 + col];
+            dov = g.dout[(long long)slot * g.dout_ss + (long long)y * g.dout_sy + (long long)j * g.ld_o + c0 + col];
         }
-        {
-            // head kernel W_L [H][nout] (nout <= 8): unguarded loads (past H*nout: 0), then stores
-            const rsrc_t rH = make_rsrc(P + g.w_off[L], (long long)H * nout);
-            float hv[8];
+        const rsrc_t rH = make_rsrc(P + g.w_off[L], (long long)H * nout);
+        float hv[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) hv[q] = bload1(rH, (tid + q * NT) * 4, 0);
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-                if (tid + q * NT < H * nout) scr[tid + q * NT] = hv[q];
-        }
-        __syncthreads();
-
-        // head kernel grad partials (thread = feature): sum_col G_{L-1}[k][col] dout[j][col]
+        for (int j = 0; j < 8; ++j) hv[j] = bload1(rH, (tid * nout + j) * 4, 0);
+        float gv[NC];
         if (gp) {
-            const float* __restrict__ gr = g.Ghead + so + (long long)tid * g.ld_s;
-            float gv[NC];
+            const rsrc_t rG = make_rsrc(g.Ghead + so, (long long)H * g.ld_s);
 #pragma unroll
             for (int q = 0; q < NC / 4; ++q) {
-                const float4 t4 = *reinterpret_cast<const float4*>(gr + 4 * q);
+                const float4 t4 = bload4(rG, tid * g.ld_s + 4 * q);
                 gv[4 * q] = t4.x; gv[4 * q + 1] = t4.y; gv[4 * q + 2] = t4.z; gv[4 * q + 3] = t4.w;
             }
+        }
+        load_first();
+        if (dl) dos[tid / NC][tid % NC] = dov;  // 0 for outputs j >= nout
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hv[j] = j < nout ? hv[j] : 0.f;
+        reinterpret_cast<float4*>(scr)[2 * tid] = float4{hv[0], hv[1], hv[2], hv[3]};
+        reinterpret_cast<float4*>(scr)[2 * tid + 1] = float4{hv[4], hv[5], hv[6], hv[7]};
+        stamp(40);
+        __syncthreads();
+        stamp(41);
+        if (gp) {
             for (int j = 0; j < nout; ++j) {
                 float v = 0.f;
 #pragma unroll
@@ -2369,18 +2380,27 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
                 part[w5 + tid * nout + j] = v;
             }
         }
+        stamp(42);
+        // dh = W_L dout: branch-free over the 8 padded outputs (the padding adds exact zeros),
+        // every LDS read of the 16 features issued before the first FMA
+        float dj[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dj[j] = dos[j][li];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const int f = 64 * w + 16 * lk + 4 * r + c;
+                const float4 wa = reinterpret_cast<const float4*>(scr)[2 * f];
+                const float4 wb = reinterpret_cast<const float4*>(scr)[2 * f + 1];
+                const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
                 float s = 0.f;
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (j < nout) s += scr[f * nout + j] * dos[j][li];
+                for (int j = 0; j < 8; ++j) s = fmaf(wv[j], dj[j], s);
                 dh[r][c] = s;
             }
         __syncthreads();  // scr (head kernel image) is reused by the first epilogue
+        stamp(43);
     }
     // parameter-grad partials, thread = feature: sums over the block's 16 columns of an LDS image
     auto row_sum = [&](const float* a, int tid_) {

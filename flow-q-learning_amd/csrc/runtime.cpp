@@ -482,6 +482,15 @@ void init_member(fqlpop* h, int slot, uint64_t seed) {
 }
 
 // ------------------------------------------------------------- DAG helpers
+// the network whose backward the phase probe stamps (diagnostic builds): FQLPOP_PHASE_NET =
+// bc / os, else the critic
+const NetLayout* phase_net(const fqlpop* h) {
+    const char* v = diag_env("FQLPOP_PHASE_NET");
+    if (v != nullptr && std::strcmp(v, "bc") == 0) return &h->bc;
+    if (v != nullptr && std::strcmp(v, "os") == 0) return &h->os;
+    return &h->critic;
+}
+
 struct Ctx {
     fqlpop* h;
     int nz;
@@ -703,7 +712,7 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         a.da = ig->da.p; a.da_ss = ig->da.ss; a.da_sy = (long long)ig->A * ig->M;
         a.ld_da = ig->M; a.D0 = ig->D; a.na = ig->A;
     }
-    if (&N == &h->critic && h->phase_dev != nullptr) {
+    if (h->phase_dev != nullptr && &N == phase_net(h)) {
         ARGCHK((long long)(M / 16) * N.E * c.nz <= h->phase_blocks, "phase probe: too many blocks");
         a.phase = h->phase_dev;
     }
@@ -926,11 +935,13 @@ double dominant_flops(const fqlpop* h) {
     return 2.0 * H * B * H * h->nz;
 }
 
-// FQLPOP_PHASE_PROBE: mean phase durations (us) of the critic backward's last launch, from
-// wave 0's stamps of every block (s_memrealtime, 100 MHz)
-void phase_report(const unsigned long long* ph, long long nb, int L) {
+// FQLPOP_PHASE_PROBE: mean phase durations (us) of the probed backward's last launch (the
+// critic's, or FQLPOP_PHASE_NET=bc / os), from wave 0's stamps of every block (s_memrealtime,
+// 100 MHz).  The actor variant (no LayerNorm) stamps only the layer start, the slab barrier
+// exit and the product end.
+void phase_report(const unsigned long long* ph, long long nb, int L, bool ln, const char* name) {
     long long t0 = -1, t1 = 0, n = 0;
-    double blk = 0, pro = 0, tail = 0, pass1[8] = {}, wait2[8] = {}, p2[8] = {}, prod[8] = {};
+    double blk = 0, pro = 0, tail = 0, pass1[8] = {}, wait2[8] = {}, p2[8] = {}, prod[8] = {}, hp[4] = {};
     for (long long b = 0; b < nb; ++b) {
         const unsigned long long* p = ph + b * SB_PHASE_STRIDE;
         if (p[0] == 0 || p[1] < p[0]) continue;
@@ -940,23 +951,36 @@ void phase_report(const unsigned long long* ph, long long nb, int L) {
         blk += (double)(p[1] - p[0]);
         pro += (double)(p[2] - p[0]);
         tail += (double)(p[1] - p[2 + 5 * (L - 1) + 3]);
+        if (p[40] != 0)  // the general head's prologue (nout > 1): W_L / dout staged, barrier, head grads, barrier
+            for (int i = 0; i < 4; ++i) hp[i] += (double)(p[40 + i] - (i == 0 ? p[0] : p[39 + i]));
         for (int i = 0; i < L && i < 8; ++i) {
             const unsigned long long* q = p + 2 + 5 * i;
-            pass1[i] += (double)(q[1] - q[0]);
-            wait2[i] += (double)(q[2] - q[1]);
-            p2[i] += (double)(q[3] - q[2]);
+            if (ln) {
+                pass1[i] += (double)(q[1] - q[0]);
+                wait2[i] += (double)(q[2] - q[1]);
+                p2[i] += (double)(q[3] - q[2]);
+            } else {
+                p2[i] += (double)(q[3] - q[0]);
+            }
             if (i + 1 < L) prod[i] += (double)(q[4] - q[3]);
         }
     }
     if (n == 0) return;
     const double us = 0.01 / (double)n;  // 100 MHz ticks -> us, averaged over blocks
     std::fprintf(stderr,
-                 "phase probe (critic backward, last launch): %lld blocks, span %.1f us, block %.2f us "
+                 "phase probe (%s backward, last launch): %lld blocks, span %.1f us, block %.2f us "
                  "(prologue %.2f, after the last slab barrier %.2f)\n",
-                 n, (double)(t1 - t0) * 0.01, blk * us, pro * us, tail * us);
+                 name, n, (double)(t1 - t0) * 0.01, blk * us, pro * us, tail * us);
+    if (hp[0] > 0)
+        std::fprintf(stderr, "  prologue: head operands staged %.2f | barrier %.2f | head grads %.2f | dh + barrier %.2f\n",
+                     hp[0] * us, hp[1] * us, hp[2] * us, hp[3] * us);
     for (int i = 0; i < L && i < 8; ++i)
-        std::fprintf(stderr, "  pass %d: LN pass 1 %.2f | stats barrier %.2f | pass 2 + du + slab barrier %.2f | dX product %.2f\n",
-                     i, pass1[i] * us, wait2[i] * us, p2[i] * us, prod[i] * us);
+        if (ln)
+            std::fprintf(stderr, "  pass %d: LN pass 1 %.2f | stats barrier %.2f | pass 2 + du + slab barrier %.2f | dX product %.2f\n",
+                         i, pass1[i] * us, wait2[i] * us, p2[i] * us, prod[i] * us);
+        else
+            std::fprintf(stderr, "  pass %d: GELU' + du + slab barrier (+ dQ/da at pass %d) %.2f | dX product %.2f\n",
+                         i, L - 1, p2[i] * us, prod[i] * us);
 }
 
 // FQLPOP_PHASE_PROBE: the persistent Euler launch's mean per-layer phases (us) over its steps
@@ -1685,7 +1709,9 @@ int fqlpop_destroy(fqlpop_t* h) {
                     std::fclose(fp);
                 }
             }
-            phase_report(h->phase_host, h->phase_blocks, h->L);
+            const NetLayout* pn = phase_net(h);
+            phase_report(h->phase_host, h->phase_blocks, h->L, pn->ln,
+                         pn == &h->critic ? "critic" : pn == &h->bc ? "BC" : "one-step");
             (void)hipHostFree(h->phase_host);
         }
         if (h->ephase_host) {
