@@ -104,10 +104,10 @@ def _pci_sysfs(device_index: int):
 
 
 def gpu_clock_power(device_index: int) -> dict:
-    """Current shader clock (MHz), power (W) and power cap (W) of the GPU from sysfs /
+    """Current shader, memory and fabric clocks (MHz), power (W) and power cap (W) of the GPU from sysfs /
     hwmon: microsecond reads, so the timed region's edges stay busy-clocked.  Values the
     box does not expose are null."""
-    out = {"sclk_mhz": None, "power_w": None, "power_cap_w": None}
+    out = {"sclk_mhz": None, "mclk_mhz": None, "fclk_mhz": None, "power_w": None, "power_cap_w": None}
     d = _pci_sysfs(device_index)
     if d is None:
         out["error"] = "no sysfs PCI node for the device"
@@ -120,12 +120,12 @@ def gpu_clock_power(device_index: int) -> dict:
         except OSError:
             return None
 
-    txt = rd(os.path.join(d, "pp_dpm_sclk"))
-    if txt:
-        for line in txt.splitlines():
+    for key, name in (("sclk_mhz", "pp_dpm_sclk"), ("mclk_mhz", "pp_dpm_mclk"), ("fclk_mhz", "pp_dpm_fclk")):
+        txt = rd(os.path.join(d, name))  # the DPM level marked "*" is the current one
+        for line in (txt or "").splitlines():
             if line.strip().endswith("*"):
                 try:
-                    out["sclk_mhz"] = int(line.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz"))
+                    out[key] = int(line.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz"))
                 except (IndexError, ValueError):
                     pass
     hw_root = os.path.join(d, "hwmon")

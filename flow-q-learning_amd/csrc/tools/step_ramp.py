@@ -56,7 +56,9 @@ def main():
         pop.step(chunk)
         pop.sync()
         el = time.perf_counter() - t0
-        print(f"{tag} {chunk} steps: {1e3 * el / chunk:.4f} ms/step  {16 * chunk / el:.1f} member-steps/s", flush=True)
+        c = bench.gpu_clock_power(0)
+        print(f"{tag} {chunk} steps: {1e3 * el / chunk:.4f} ms/step  {16 * chunk / el:.1f} member-steps/s  "
+              f"sclk {c['sclk_mhz']} mclk {c['mclk_mhz']} fclk {c['fclk_mhz']} {c['power_w']} W", flush=True)
 
     for i in range(n_chunks):
         timed(f"chunk {i:2d}")
