@@ -91,7 +91,6 @@ struct AdamEpi {
                                       // 3 = no W^T pass
     int nt;                           // non-temporal optimiser streams: 1 m/v, 2 target, 4 p_in, 8 p_out/W^T
     int stagger;                      // first-wave start offsets (s_sleep 32 units per co-resident rank), 0 = off
-    int persist;                      // tile 14 (wave-specialised launch): persistent blocks, 0 = 2 per CU
     // the net's small leaves (biases, LN, head) ride in the same launch: blocks past the
     // GEMM tiles run the adam_kernel body on small.ids chunks (small_blocks = chunks x nz)
     AdamArgs small;
@@ -105,8 +104,7 @@ struct GemmGroupArgs {
 };
 // tile: 2 = 64x128, 3 = 128x128 (others 64x64 / 128x64); adam != null: fused
 // optimiser epilogue (tile 2 or 3 only), else plain stores into g[i].C; with adam: 6 / 10 =
-// 64x128 at BK 16 (3 / 4 blocks per CU), 14 = the same tiles in the wave-specialised
-// persistent launch (dwopt_ws_kernel, K a multiple of 16, every problem with the same K)
+// 64x128 at BK 16 (3 / 4 blocks per CU)
 void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, const AdamEpi* adam = nullptr);
 // tiles per problem of the grouped dW launch (stats chunks of a fused W leaf)
 int gemm_group_tiles(int tile, int M, int N);

@@ -58,13 +58,6 @@ DEV float wave_min(float v) {
     return v;
 }
 
-// an opaque copy of v (the compiler cannot hoist what is computed from it; dwopt_ws_kernel's
-// per-unit W^T addresses)
-DEV int opq(int v) {
-    asm volatile("" : "+v"(v));
-    return v;
-}
-
 // the lane id (0..63) from v_mbcnt, in volatile asm: recomputed where it is used, never
 // hoisted (and so never spilled) by the compiler
 DEV int lane_id_asm() {
@@ -726,331 +719,6 @@ __global__ __launch_bounds__(256, 4) void gemm_group_kernel_o4(const GemmGroupAr
     gemm_group_body<BM, BN, ARC, BRC, EPI, BK>(ga, smem);
 }
 
-// ---------------------------------------------- wave-specialised dW + optimiser ----
-// The same work as gemm_group_kernel_o4<64, 128, true, true, EPI_ADAM, 16> (tile id 14),
-// bit-identical, in a persistent launch whose blocks split their 8 waves into two groups
-// that run concurrently:
-//   G (waves 0-3): the dW product of tile n, gemm_body's k-loop (operand slices staged through
-//                  LDS in the KB layout, double-buffered, the same MFMA sequence);
-//   O (waves 4-7): optax.adam / the target EMA / grad stats and the W^T copy of tile n - 1
-//                  from the gradient tile G left in LDS, with the p / m / v / target loads of
-//                  the next WS_D units always in flight (across tiles).
-// Inside a tile period each group synchronises only its own 4 waves (ws_group_sync: an LDS
-// arrival counter, so a G k-slice never waits for the optimiser and vice versa); the period
-// ends in two block barriers: A (O is done with the gradient tile), G writes its
-// accumulators into it, B (published).  In the one-tile-per-block launch every co-resident
-// block ran its k-loop, then its HBM-bound optimiser pass, at the same time as the others
-// (they start together), so the two phases hardly overlapped.
-constexpr int WS_BM = 64, WS_BN = 128, WS_BK = 16, WS_PT = WS_BN + 1, WS_NU = 8, WS_D = 3;
-constexpr int WS_RP = rc_pitch<WS_BK, true>();
-constexpr int WS_STAGE = (WS_BM + WS_BN) * WS_RP;  // one A + B slice
-constexpr int WS_SMEM = WS_BM * WS_PT + 2 * WS_STAGE + 16;
-
-DEV void ws_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// barrier of one 4-wave group: each wave's LDS writes complete, then it counts itself in
-// and waits for the group's 4 arrivals (*ctr counts up by 4 per sync; target = 4 x syncs)
-DEV void ws_group_sync(unsigned* ctr, unsigned target) {
-    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
-}
-
-// block-uniform description of logical tile lt of a grouped launch
-struct WsTile {
-    int gi, slot, y, tile, per, i0, j0;
-};
-DEV WsTile ws_tile(const GemmGroupArgs& ga, int lt) {
-    int gi = 0;
-#pragma unroll
-    for (int i = 1; i < GEMM_GROUP_MAX; ++i)
-        if (i < ga.ng && lt >= ga.first[i]) gi = i;
-    gi = uni(gi);
-    const GemmArgs& g = ga.g[gi];
-    const int gM = uni(g.M), gN = uni(g.N), gny = uni(g.ny);
-    const int tiles_m = gM / WS_BM + (gM % WS_BM != 0), tiles_n = gN / WS_BN;
-    const int per = tiles_m * tiles_n, w = lt - uni(ga.first[gi]);
-    const int tile = w % per, yz = w / per;
-    WsTile t;
-    t.gi = gi; t.per = per; t.tile = tile;
-    t.y = yz % gny;
-    t.slot = uni(g.slots[yz / gny]);
-    t.i0 = (tile / tiles_n) * WS_BM;
-    t.j0 = (tile % tiles_n) * WS_BN;
-    return t;
-}
-
-__global__ __launch_bounds__(512, 4) void dwopt_ws_kernel(const GemmGroupArgs ga) {
-    __shared__ __attribute__((aligned(16))) float smem[WS_SMEM];
-    constexpr int BM = WS_BM, BN = WS_BN, BK = WS_BK, PT = WS_PT, RP = WS_RP, NU = WS_NU, D = WS_D;
-    const int nper = ga.adam.persist;  // persistent blocks (a multiple of 8)
-    if ((int)blockIdx.x >= nper) {
-        const int sb = blockIdx.x - nper, nch = ga.adam.small.n_chunks;
-        adam_chunk_t<512>(ga.adam.small, sb % nch, sb / nch);
-        return;
-    }
-    const int T = ga.first[ga.ng];
-    // the XCD's contiguous range of logical tiles (as xcd_remap), dealt round-robin to its blocks
-    const int q8 = T >> 3, r8 = T & 7, x = blockIdx.x & 7, jb = blockIdx.x >> 3, nbx = nper >> 3;
-    const int start = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
-    const int cnt = q8 + (x < r8 ? 1 : 0);
-    const int ntl = jb < cnt ? (cnt - jb + nbx - 1) / nbx : 0;
-    if (ntl == 0) return;
-    auto tile_id = [&](int n) { return start + jb + n * nbx; };
-    const int gK = uni(ga.g[0].K);  // one net: every problem has K = Mg
-    const int nk = gK / BK;
-    float* const Gt = smem;                            // the gradient tile [BM][PT]
-    float* const stage = smem + BM * PT;               // G: [2][A BM x RP | B BN x RP]
-    float* const red = stage + 2 * WS_STAGE;           // O: [12] wave stats partials
-    unsigned* const ctr = reinterpret_cast<unsigned*>(red + 12);  // [2] group arrival counters
-    const AdamEpi& e = ga.adam;
-    const int wave = threadIdx.x >> 6;
-    if (threadIdx.x < 2) ctr[threadIdx.x] = 0u;
-    ws_barrier();
-
-    if (wave < 4) {
-        // ------------------------------------------------------------ G: the dW products
-        const int tid = threadIdx.x, lane = tid & 63;
-        const int wi = (wave >> 1) * (BM / 2), wj = (wave & 1) * (BN / 2);
-        const int l32 = lane & 31, lh = lane >> 5;
-        unsigned syncs = 0;
-        struct Src {
-            rsrc_t rA, rB;
-            int lda, ldb, i0, j0;
-        };
-        auto src = [&](const WsTile& tt) {
-            const GemmArgs& g = ga.g[tt.gi];
-            const int gM = uni(g.M), gN = uni(g.N);
-            Src r;
-            r.lda = uni(g.lda);
-            r.ldb = uni(g.ldb);
-            r.rA = make_rsrc(uniptr(at(g.A, tt.slot, tt.y)), (long long)(gM - 1) * r.lda + gK);
-            r.rB = make_rsrc(uniptr(at(g.B, tt.slot, tt.y)), (long long)(gN - 1) * r.ldb + gK);
-            r.i0 = tt.i0;
-            r.j0 = tt.j0;
-            return r;
-        };
-        // slice staging, as gemm_body: 1 A + 2 B float4 per thread, KB layout (pitch RP); two
-        // register sets, set s & 1 holding slice s (slices numbered on across tiles), so a
-        // slice's loads have two k-slices of MFMAs to land in
-        float4 ra[2], rb[2][2];
-        auto load = [&](int set, const Src& r, int k0) {
-            ra[set] = stage_load<BM, BK, true>(r.rA, r.lda, 0, r.i0, k0);
-            rb[set][0] = stage_load<BN, BK, true>(r.rB, r.ldb, 0, r.j0, k0);
-            rb[set][1] = stage_load<BN, BK, true>(r.rB, r.ldb, 1, r.j0, k0);
-        };
-        auto store = [&](int set, int buf) {
-            float* S = stage + buf * WS_STAGE;
-            stage_store<BM, BK, true, RP>(S, 0, ra[set]);
-            stage_store<BN, BK, true, RP>(S + BM * RP, 0, rb[set][0]);
-            stage_store<BN, BK, true, RP>(S + BM * RP, 1, rb[set][1]);
-        };
-        // one k-slice: loads of slice kt + 2 (or the next tile's) into set kt & 1, MFMAs
-        // on LDS buffer kt & 1, then slice kt + 1 from set (kt + 1) & 1 into the other buffer
-        auto step = [&](f32x16 (&acc)[2], int kt, int set, const Src& sr, const Src& srn) {
-            {  // selected, not branched: loads on both sides of a branch get
-               // over-conservative vmcnt waits after the join
-                const bool in = kt + 2 < nk;
-                Src sx;
-                sx.rA = in ? sr.rA : srn.rA;
-                sx.rB = in ? sr.rB : srn.rB;
-                sx.lda = in ? sr.lda : srn.lda;
-                sx.ldb = in ? sr.ldb : srn.ldb;
-                sx.i0 = in ? sr.i0 : srn.i0;
-                sx.j0 = in ? sr.j0 : srn.j0;
-                load(set, sx, (in ? kt + 2 : kt + 2 - nk) * BK);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            const float* S = stage + set * WS_STAGE;
-            float av[8], bv[8][2];
-            {
-                const float* r = S + (wi + l32) * RP + 8 * lh;
-                const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
-                av[0] = x0.x; av[1] = x0.y; av[2] = x0.z; av[3] = x0.w;
-                av[4] = x1.x; av[5] = x1.y; av[6] = x1.z; av[7] = x1.w;
-            }
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const float* r = S + BM * RP + (wj + b * 32 + l32) * RP + 8 * lh;
-                const float4 x0 = *reinterpret_cast<const float4*>(r), x1 = *reinterpret_cast<const float4*>(r + 4);
-                bv[0][b] = x0.x; bv[1][b] = x0.y; bv[2][b] = x0.z; bv[3][b] = x0.w;
-                bv[4][b] = x1.x; bv[5][b] = x1.y; bv[6][b] = x1.z; bv[7][b] = x1.w;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int kk = 0; kk < 8; ++kk)
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-                    acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk][b], acc[b], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (kt + 1 < nk) {
-                store(set ^ 1, set ^ 1);
-                ws_group_sync(ctr, syncs += 4);
-            }
-        };
-        {
-            const WsTile t0 = ws_tile(ga, tile_id(0));
-            const Src s0 = src(t0);
-            load(0, s0, 0);
-            load(1, s0, BK);
-        }
-        Src sr = src(ws_tile(ga, tile_id(0)));
-        for (int it = 0; it <= ntl; ++it) {  // + 1 period: O's pass over the last tile
-            f32x16 acc[2];
-            if (it < ntl) {
-                const bool more = it + 1 < ntl;
-                const Src srn = more ? src(ws_tile(ga, tile_id(it + 1))) : sr;
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-                store(0, 0);  // slice 0 (buffer 0 was last read two slices ago, before a sync)
-                ws_group_sync(ctr, syncs += 4);
-#if defined(FQ_WS_SKIP) && FQ_WS_SKIP == 1
-                for (int kt = 0; kt < 0; kt += 2) {
-#else
-                for (int kt = 0; kt < nk; kt += 2) {
-#endif
-                    step(acc, kt, 0, sr, srn);
-                    step(acc, kt + 1, 1, sr, srn);
-                }
-                sr = srn;
-            }
-            ws_barrier();  // A: O is done with the gradient tile (tile it - 1)
-            if (it < ntl) {
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        Gt[(wi + (r & 3) + 8 * (r >> 2) + 4 * lh) * PT + wj + b * 32 + l32] = acc[b][r];
-            }
-            ws_barrier();  // B: gradient tile it published
-        }
-        return;
-    }
-
-    // ------------------------------------------------------------ O: the optimiser
-    const int otid = threadIdx.x - 256, ow = wave - 4;
-    constexpr int TPR = BN / 4;  // 32 threads per row, 8 rows per unit
-    const int cj = (otid % TPR) * 4, ri = otid / TPR;
-    const float lr = e.lr, tau = e.tau;
-    unsigned syncs = 0;
-    struct Res {
-        rsrc_t rP, rPo, rM, rV, rT;
-        int gM, ldc;
-        bool hasT;
-    };
-    auto tile_res = [&](const WsTile& tt) {
-        const GemmArgs& g = ga.g[tt.gi];
-        Res rs;
-        rs.gM = uni(g.M);
-        rs.ldc = uni(g.ldc);
-        const long long pb = uni64((long long)tt.slot * e.P + e.w_off[tt.gi] + (long long)tt.y * e.ens);
-        const long long nleaf = (long long)rs.gM * rs.ldc;
-        rs.rP = make_rsrc(e.p_in + pb, nleaf);
-        rs.rPo = make_rsrc(e.p_out + pb, nleaf);
-        rs.rM = make_rsrc(e.m + pb, nleaf);
-        rs.rV = make_rsrc(e.v + pb, nleaf);
-        rs.hasT = e.target != nullptr;
-        rs.rT = make_rsrc(uniptr(rs.hasT ? e.target + (long long)tt.slot * e.PT + e.w_off[tt.gi] + (long long)tt.y * e.ens
-                                         : e.m + pb), nleaf);
-        return rs;
-    };
-    // unit u of a tile (rows 8 u + ri, columns cj .. cj + 3) in slot u % (D + 1): 8 units per
-    // tile, a multiple of D + 1, so a unit's slot is the same in every tile
-    float4 p4[D + 1], m4[D + 1], v4[D + 1], t4[D + 1];
-    auto issue = [&](const Res& rs, const WsTile& tt, int u, int q) {
-        const int off = ((tt.i0 + u * 8 + ri) * rs.ldc + tt.j0 + cj) * 4;
-        p4[q] = bload4_aux(rs.rP, off, 0);
-        m4[q] = bload4_aux(rs.rM, off, 1);
-        v4[q] = bload4_aux(rs.rV, off, 1);
-        t4[q] = rs.hasT ? bload4_aux(rs.rT, off, 1) : float4{0.f, 0.f, 0.f, 0.f};
-    };
-    static_assert(NU % (D + 1) == 0, "unit slots must repeat per tile");
-    WsTile ta = ws_tile(ga, tile_id(0));  // the tile of the next pass
-    Res ra = tile_res(ta);
-#pragma unroll
-    for (int u = 0; u < D; ++u) issue(ra, ta, u, u);
-    ws_barrier();  // A (period 0: G's first k-loop)
-    ws_barrier();  // B
-    for (int it = 1; it <= ntl; ++it) {
-        // tile it - 1: optax.adam / EMA / stats from the gradient tile, the new p back into it;
-        // the loads of the next D units are in flight throughout (the last D of them belong
-        // to tile it)
-#if !(defined(FQ_WS_SKIP) && FQ_WS_SKIP == 2)
-        const bool more = it < ntl;
-        const WsTile tn = more ? ws_tile(ga, tile_id(it)) : ta;
-        const Res rn = more ? tile_res(tn) : ra;
-        const float tc = (float)(e.count[ta.slot] + 1);
-        const float bc1 = 1.0f - powf(0.9f, tc), bc2 = 1.0f - powf(0.999f, tc);
-        const float rbc1 = 1.0f / bc1, rbc2 = 1.0f / bc2;
-        const int rows = min(BM, ra.gM - ta.i0);
-        float mx = -INFINITY, mn = INFINITY, ss = 0.f;
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-            const int q = u % (D + 1);
-            const int i = u * 8 + ri;
-            const int off = ((ta.i0 + i) * ra.ldc + ta.j0 + cj) * 4;
-            const bool live = i < rows;
-            float* gs = Gt + i * PT + cj;
-            float pp[4] = {p4[q].x, p4[q].y, p4[q].z, p4[q].w};
-            float mm[4] = {m4[q].x, m4[q].y, m4[q].z, m4[q].w};
-            float vv[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
-            float tt[4] = {t4[q].x, t4[q].y, t4[q].z, t4[q].w};
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float gr = gs[c];
-                adam_moments(gr, mm[c], vv[c]);
-                tt[c] = ema_target(pp[c], tt[c], tau);
-                pp[c] = adam_step_fast(pp[c], mm[c], vv[c], rbc1, rbc2, lr);
-                gs[c] = pp[c];
-                mx = live ? fmaxf(mx, gr) : mx;
-                mn = live ? fminf(mn, gr) : mn;
-                ss = live ? fmaf(gr, gr, ss) : ss;
-            }
-            // the slot is free: the unit D ahead (this tile's, or the next one's)
-            if (u + D < NU) issue(ra, ta, u + D, (u + D) % (D + 1));
-            else if (more) issue(rn, tn, u + D - NU, (u + D) % (D + 1));
-            bstore4_aux(ra.rPo, float4{pp[0], pp[1], pp[2], pp[3]}, off, 0);
-            bstore4_aux(ra.rM, float4{mm[0], mm[1], mm[2], mm[3]}, off, 1);
-            bstore4_aux(ra.rV, float4{vv[0], vv[1], vv[2], vv[3]}, off, 1);
-            if (ra.hasT) bstore4_aux(ra.rT, float4{tt[0], tt[1], tt[2], tt[3]}, off, 1);
-            // fold the stats chains in this unit (the compiler otherwise keeps every unit's
-            // gradient values live to the end)
-            asm volatile("" : "+v"(mx), "+v"(mn), "+v"(ss));
-        }
-        mx = wave_max(mx);
-        mn = wave_min(mn);
-        ss = wave_sum(ss);
-        if ((otid & 63) == 0) {
-            red[ow] = mx;
-            red[4 + ow] = mn;
-            red[8 + ow] = ss;
-        }
-        ws_group_sync(ctr + 1, syncs += 4);  // the new p of every row, the stats partials
-        if (otid == 0) {
-            float* st = e.stats + ((long long)ta.slot * e.n_total_chunks + e.stat_base[ta.gi] + ta.y * ta.per + ta.tile) * 3;
-            st[0] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-            st[1] = fminf(fminf(red[4], red[5]), fminf(red[6], red[7]));
-            st[2] = red[8] + red[9] + red[10] + red[11];
-        }
-        if (e.wt_off[ta.gi] >= 0) {
-            float* __restrict__ WT = e.wt_out + (long long)ta.slot * e.PTT + e.wt_off[ta.gi] + (long long)ta.y * e.wt_sy;
-            constexpr int TPC = BM / 4;
-            for (int q = opq(otid); q < BM * BN / 4; q += 256) {
-                const int jj = q / TPC, ii = (q % TPC) * 4;
-                const float* g4 = Gt + ii * PT + jj;
-                *reinterpret_cast<float4*>(WT + (long long)(ta.j0 + jj) * ra.gM + ta.i0 + ii) =
-                    float4{g4[0], g4[PT], g4[2 * PT], g4[3 * PT]};
-            }
-        }
-        ta = tn;
-        ra = rn;
-#endif
-        ws_barrier();  // A
-        ws_barrier();  // B
-    }
-}
-
 int gemm_group_tiles(int tile, int M, int N) {
     const int bm = (tile & 1) ? 128 : 64, bn = (tile & 2) ? 128 : 64;
     return ((M + bm - 1) / bm) * (N / bn);
@@ -1066,21 +734,6 @@ void launch_gemm_group_dw(int tile, const GemmArgs* gs, int ng, hipStream_t s, c
     }
     ga.first[ng] = tot;
     ga.ng = ng;
-    bool ws_ok = true;  // the wave-specialised launch: one K for all problems, K % 32 == 0
-    for (int i = 0; i < ng; ++i) ws_ok = ws_ok && gs[i].K == gs[0].K && gs[i].K % 32 == 0;
-    if (adam && tile == 14 && !ws_ok) {  // its tiles, i.e. its stats chunks, are tile 10's
-        tile = 10;
-    }
-    if (adam && tile == 14) {
-        // wave-specialised persistent launch: 2 blocks per CU over the tiles, then the
-        // small-leaf blocks
-        ga.adam = *adam;
-        const int want = adam->persist > 0 ? adam->persist : 512, cap = 8 * ((tot + 7) / 8);
-        const int per = want < cap ? want : cap;
-        ga.adam.persist = per;
-        hipLaunchKernelGGL(dwopt_ws_kernel, dim3(per + adam->small_blocks), dim3(512), 0, s, ga);
-        return;
-    }
     if (adam) {
         ga.adam = *adam;
         tot += adam->small_blocks;

@@ -78,7 +78,6 @@ struct EngineOptions {
     int dw_tile_critic = 10, dw_tile_actor = 10;  // grouped dW tile ids (launch_gemm_group_dw)
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
     int dw_stagger = 0;    // fused dW + optimiser: first-wave start offsets (AdamEpi::stagger)
-    int dw_persist = 0;    // tile 14: persistent blocks of the wave-specialised launch (0: 2 per CU)
 };
 EngineOptions g_engine_opts;
 
@@ -92,11 +91,10 @@ const EngineOptionRef kEngineOptions[] = {
     {"stream_bwd", &EngineOptions::stream_bwd, 0, 1},   {"fused_adam", &EngineOptions::fused_adam, 0, 1},
     {"cdw_sb", &EngineOptions::cdw_sb, 0, 1},           {"serial", &EngineOptions::serial, 0, 1},
     {"streams", &EngineOptions::streams, 3, 4},         {"prio", &EngineOptions::prio, 0, 2},
-    {"dw_tile_critic", &EngineOptions::dw_tile_critic, 0, 14},
-    {"dw_tile_actor", &EngineOptions::dw_tile_actor, 0, 14},
+    {"dw_tile_critic", &EngineOptions::dw_tile_critic, 0, 10},
+    {"dw_tile_actor", &EngineOptions::dw_tile_actor, 0, 10},
     {"adam_nt", &EngineOptions::adam_nt, 0, 3},
     {"dw_stagger", &EngineOptions::dw_stagger, 0, 256},
-    {"dw_persist", &EngineOptions::dw_persist, 0, 1 << 20},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -781,7 +779,6 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
             // (+1.0 % same-box; engine option adam_nt: bit mask, see AdamEpi::nt)
             ae.nt = h->opt.adam_nt;
             ae.stagger = h->opt.dw_stagger;
-            ae.persist = h->opt.dw_persist;
         }
         ae.small = adam_args(c, ni);
         ae.small_blocks = ae.small.n_chunks * c.nz;

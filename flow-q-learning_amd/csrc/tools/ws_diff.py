@@ -1,7 +1,7 @@
 """Which leaves differ between two engine-option sets after n device-sampled steps
 (developer tool for bit-identity checks of alternate kernels).
 
-  python ws_diff.py "dw_tile_critic=14,dw_tile_actor=14" [steps] [H] [B]
+  python ws_diff.py "dw_tile_critic=6,dw_tile_actor=6" [steps] [H] [B]
 """
 import os
 import sys

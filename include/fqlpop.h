@@ -78,9 +78,8 @@ const char* fqlpop_last_error(void);
  * (bit-identical, or the per-layer / unfused paths within the parity tolerance),
  * for tests and profiling; there is no reference counterpart.  Names:
  *   euler_fused, stream_fwd, stream_bwd, fused_adam, cdw_sb, serial  (0/1)
- *   streams (3/4), prio (0..2), dw_tile_critic / dw_tile_actor (0..14), adam_nt (0..3),
- *   dw_stagger (0..256: start offsets of the fused dW + optimiser launch's first blocks),
- *   dw_persist (blocks of the wave-specialised dW launch, tile 14; 0 = 2 per CU).
+ *   streams (3/4), prio (0..2), dw_tile_critic / dw_tile_actor (0..10), adam_nt (0..3),
+ *   dw_stagger (0..256: start offsets of the fused dW + optimiser launch's first blocks).
  * The defaults are the measured-fastest configuration.  Unknown names or values
  * out of range: FQLPOP_E_ARG.  The production library reads no environment
  * variable; result-changing timing switches exist only in diagnostic builds. */

@@ -331,12 +331,11 @@ def _sampled_run_now(H, B, steps):
 
 
 # (the fused dW + optimiser runs at H = 512 only: the streamed backward needs it)
-@pytest.mark.parametrize("H,B,tile", [(512, 256, 6), (512, 64, 6), (512, 256, 14), (512, 64, 14), (512, 1024, 14)])
+@pytest.mark.parametrize("H,B,tile", [(512, 256, 6), (512, 64, 6)])
 def test_fused_dw_optimiser_variants_bit_identical(H, B, tile):
-    """The fused dW + optimiser launch at 4 blocks per CU (tile 10, the default), at 3
-    (tile 6) and the wave-specialised persistent launch (tile 14: MFMA waves on tile n
-    beside optimiser waves on tile n-1) run the same arithmetic: parameters, Adam state,
-    target and grad stats are bit-identical after several device-sampled steps."""
+    """The fused dW + optimiser launch at 4 blocks per CU (tile 10, the default) and at 3
+    (tile 6) run the same arithmetic: parameters, Adam state, target and grad stats are
+    bit-identical after several device-sampled steps."""
     ref = _sampled_run(H, B, 3, {"dw_tile_critic": tile, "dw_tile_actor": tile})
     got = _sampled_run(H, B, 3, {})
     assert np.array_equal(got[0], ref[0])
