@@ -1,6 +1,6 @@
 """Step rate right after setup, in chunks (developer tool, on the GPU box):
 
-  python flow-q-learning_amd/csrc/tools/step_ramp.py [chunk] [n_chunks] [idle_s] [preheat_ms] [mem]
+  python flow-q-learning_amd/csrc/tools/step_ramp.py [chunk] [n_chunks] [idle_s] [preheat_ms] [mem] [graph|eager]
 
 (mem = 1: the preheat also streams HBM: device-to-device copies of a 1 GB buffer on a side
 stream while the dominant kernel replays)
@@ -30,12 +30,13 @@ def main():
     idle = float(sys.argv[3]) if len(sys.argv) > 3 else 1.0
     preheat_ms = float(sys.argv[4]) if len(sys.argv) > 4 else 0.0
     mem = len(sys.argv) > 5 and sys.argv[5] == "1"
+    graph = not (len(sys.argv) > 6 and sys.argv[6] == "eager")  # eager: no hipGraph replays
     torch.cuda.set_device(0)
     wl = bench.WORKLOADS["cube"]
     data = bench.synthetic_dataset(1_000_000, wl["obs_dim"], wl["action_dim"])
     alphas, seeds = bench.population_values(16)
     pop = Population(PopulationConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"],
-                                      batch_size=wl["batch_size"]), alphas, seeds, device=0)
+                                      batch_size=wl["batch_size"], use_graph=graph), alphas, seeds, device=0)
     pop.set_dataset(data)
     if preheat_ms > 0:  # as bench.py --preheat-ms
         us, _ = pop.time_dominant_kernel(1)
