@@ -162,27 +162,47 @@ DEV void dense_dx(const float* WT, const float* g, int K, int N, float* g_in, co
 
 // Partial parameter grads of one Dense over the block's rows (MFMA over the 16 rows):
 // dW[k][f] = sum_r in[k][r] g[f][r], db[f] = sum_r g[f][r]
-// (acc: added to the partials already there -- the sum over the steps of a sequence)
+// (acc: added to the partials already there -- the sum over the steps of a sequence).
+// A wave's tiles go in batches of DW_MT: with acc, the batch's old partials are loaded
+// first, all in flight together (one dependent read per tile cost one L2 round trip each,
+// 16 of them per wave in a 128 x 256 layer, at every step of a multistep sequence)
+constexpr int DW_MT = 8;
 DEV void dense_dw(const float* in, const float* g, int K, int N, float* __restrict__ pW, float* __restrict__ pb,
                   bool acc = false) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, lk = lane >> 4;
     const int tf = (N + 15) / 16, nt = (K + 15) / 16 * tf;
-    for (int t = w; t < nt; t += NT / 64) {
-        const int k0 = 16 * (t / tf), f0 = 16 * (t % tf);
-        f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int NW = NT / 64;
+    for (int t0 = w; t0 < nt; t0 += NW * DW_MT) {
+        float old[DW_MT][4];
+        if (acc) {
 #pragma unroll
-        for (int s = 0; s < R / 4; ++s) {
-            const float av = k0 + li < K ? in[(k0 + li) * R + 4 * s + lk] : 0.f;  // A[k][r]
-            const float bv = f0 + li < N ? g[(f0 + li) * R + 4 * s + lk] : 0.f;   // B[r][f]
-            d = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, d, 0, 0, 0);
+            for (int j = 0; j < DW_MT; ++j) {
+                const int t = min(t0 + NW * j, nt - 1);  // past the wave's last tile: a re-read
+                const int k0 = 16 * (t / tf), f0 = 16 * (t % tf);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = min(k0 + 4 * lk + q, K - 1), f = min(f0 + li, N - 1);  // in range
+                    old[j][q] = pW[(long long)k * N + f];
+                }
+            }
         }
-        // d[q]: k = k0 + 4lk + q, f = f0 + li
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int k = k0 + 4 * lk + q, f = f0 + li;
-            if (k < K && f < N) {
-                const long long o = (long long)k * N + f;
-                pW[o] = acc ? pW[o] + d[q] : d[q];
+        for (int j = 0; j < DW_MT; ++j) {
+            const int t = t0 + NW * j;
+            if (t >= nt) break;
+            const int k0 = 16 * (t / tf), f0 = 16 * (t % tf);
+            f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < R / 4; ++s) {
+                const float av = k0 + li < K ? in[(k0 + li) * R + 4 * s + lk] : 0.f;  // A[k][r]
+                const float bv = f0 + li < N ? g[(f0 + li) * R + 4 * s + lk] : 0.f;   // B[r][f]
+                d = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, d, 0, 0, 0);
+            }
+            // d[q]: k = k0 + 4lk + q, f = f0 + li
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = k0 + 4 * lk + q, f = f0 + li;
+                if (k < K && f < N) pW[(long long)k * N + f] = acc ? old[j][q] + d[q] : d[q];
             }
         }
     }
