@@ -104,9 +104,23 @@ DEV float softplus(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
 // [K][N]; dX: A = W^T [N][K] with mask = relu'(the layer input).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// An LDS activation pointer that went through a runtime-indexed pointer array (acts[i]) is
+// generic again: its accesses compile to flat instructions, which count in both vmcnt and
+// lgkmcnt, so every LDS read behind them also waited for the global loads and stores in
+// flight.  The assumption lets the compiler address LDS directly.
+template <typename T>
+DEV T* lds_ptr(T* p) {
+#if __HIP_DEVICE_COMPILE__  // (the builtin exists for the device pass only)
+    __builtin_assume(__builtin_amdgcn_is_shared((const void*)p));
+#endif
+    return p;
+}
 template <int KS>
 DEV void em_mfma_t(const float* __restrict__ A, const float* __restrict__ bias, const float* x, int Kr, int M,
                    float* y, bool relu, const float* mask) {
+    x = lds_ptr(x);
+    y = lds_ptr(y);
+    if (mask) mask = lds_ptr(mask);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, lk = lane >> 4;
     const int ntile = (M + 15) / 16, nks = (Kr + 3) / 4;
     // unguarded buffer loads (a guarded load compiles to a branch + vmcnt(0) wait): k >= Kr
@@ -144,20 +158,25 @@ DEV void em_mfma_t(const float* __restrict__ A, const float* __restrict__ bias, 
     }
     __syncthreads();
 }
+// KSMAX: the most k-steps a wave keeps in flight (32 = 32 VGPRs of fragments; the multistep
+// kernel, at its register limit, takes 16)
+template <int KSMAX = 32>
 DEV void em_mfma(const float* A, const float* bias, const float* x, int Kr, int M, float* y, bool relu,
                  const float* mask) {
     if (Kr <= 32) em_mfma_t<8>(A, bias, x, Kr, M, y, relu, mask);
-    else if (Kr <= 64) em_mfma_t<16>(A, bias, x, Kr, M, y, relu, mask);
+    else if (Kr <= 64 || KSMAX < 32) em_mfma_t<16>(A, bias, x, Kr, M, y, relu, mask);
     else em_mfma_t<32>(A, bias, x, Kr, M, y, relu, mask);
 }
 // out[f][r] = act(sum_k W[k][f] in[k][r] + b[f])
+template <int KSMAX = 32>
 DEV void dense_fwd(const float* W, const float* b, const float* in, int K, int N, float* out, bool relu) {
-    em_mfma(W, b, in, K, N, out, relu, nullptr);
+    em_mfma<KSMAX>(W, b, in, K, N, out, relu, nullptr);
 }
 // g_in[k][r] = sum_f W[k][f] g[f][r] (times relu'(in) when mask_in), from WT = W^T [N][K]
 // (the transposed copy the optimiser keeps)
+template <int KSMAX = 32>
 DEV void dense_dx(const float* WT, const float* g, int K, int N, float* g_in, const float* mask_in) {
-    em_mfma(WT, nullptr, g, N, K, g_in, false, mask_in);
+    em_mfma<KSMAX>(WT, nullptr, g, N, K, g_in, false, mask_in);
 }
 
 // Partial parameter grads of one Dense over the block's rows (MFMA over the 16 rows):
@@ -169,6 +188,8 @@ DEV void dense_dx(const float* WT, const float* g, int K, int N, float* g_in, co
 constexpr int DW_MT = 8;
 DEV void dense_dw(const float* in, const float* g, int K, int N, float* __restrict__ pW, float* __restrict__ pb,
                   bool acc = false) {
+    in = lds_ptr(in);
+    g = lds_ptr(g);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, lk = lane >> 4;
     const int tf = (N + 15) / 16, nt = (K + 15) / 16 * tf;
     constexpr int NW = NT / 64;
@@ -218,14 +239,15 @@ DEV void dense_dw(const float* in, const float* g, int K, int N, float* __restri
 // Frozen termination predictor on pred = tacts[0] [D][R]: weighted BCE of its logit
 // (envmodel/loss.py:14-30) into the log sums 1..5, and its input gradient, scaled by
 // tw / norm, added to gA [D][R].  inv_n: 1 / (number of scored predictions).
+template <int KSMAX = 32>
 DEV void tp_score(const StepArgs& a, float* const* tacts, float* gA, float* gB, float* gC, const float* lab,
                   float (*lsum)[R], float inv_n, float norm) {
     const Net& T = a.tpn;
     const int tid = threadIdx.x;
     for (int i = 0; i < T.n; ++i)
-        dense_fwd(a.tp + T.w[i], a.tp + T.b[i], tacts[i], T.dims[i], T.dims[i + 1], tacts[i + 1], i < T.n - 1);
+        dense_fwd<KSMAX>(a.tp + T.w[i], a.tp + T.b[i], tacts[i], T.dims[i], T.dims[i + 1], tacts[i + 1], i < T.n - 1);
     if (tid < R) {
-        const float x = tacts[T.n][tid], z = lab[tid], w = a.ttw;
+        const float x = lds_ptr(tacts[T.n])[tid], z = lab[tid], w = a.ttw;
         const float ce = softplus(x) - x * z;
         lsum[1][tid] += (z > 0.f ? w * ce : ce) / (w + 1.f);
         lsum[2][tid] += z > 0.f ? ce : 0.f;
@@ -240,11 +262,12 @@ DEV void tp_score(const StepArgs& a, float* const* tacts, float* gA, float* gB, 
     float* src = gB;
     float* dst = gC;
     for (int i = T.n - 1; i >= 0; --i) {
-        dense_dx(a.tpt + T.w[i], src, T.dims[i], T.dims[i + 1], dst, i > 0 ? tacts[i] : nullptr);
+        dense_dx<KSMAX>(a.tpt + T.w[i], src, T.dims[i], T.dims[i + 1], dst, i > 0 ? tacts[i] : nullptr);
         float* tmp = src;
         src = dst;
         dst = tmp;
     }
+    src = lds_ptr(src);
     for (int t = tid; t < a.D * R; t += NT) gA[t] += a.tw / norm * src[t];
     __syncthreads();
 }
@@ -337,15 +360,15 @@ __global__ __launch_bounds__(NT) void em_grad_kernel(const StepArgs a) {
             const int k = t / R, r = t % R;
             const float xh = (x0[t] - mu_s[r]) * rs_s[r];
             xhat[t] = xh;
-            acts[0][t] = xh * P[N.ln_scale + k] + P[N.ln_bias + k];
+            lds_ptr(acts[0])[t] = xh * P[N.ln_scale + k] + P[N.ln_bias + k];
         }
     } else {
-        for (int t = tid; t < K0 * R; t += NT) acts[0][t] = x0[t];
+        for (int t = tid; t < K0 * R; t += NT) lds_ptr(acts[0])[t] = x0[t];
     }
     __syncthreads();
     for (int i = 0; i < N.n; ++i)
         dense_fwd(P + N.w[i], P + N.b[i], acts[i], N.dims[i], N.dims[i + 1], acts[i + 1], i < N.n - 1);
-    const float* out = acts[N.n];
+    const float* out = lds_ptr(acts[N.n]);
 
     // ---- loss, output gradient (gA [dout][R]) and log sums
     const float invB = 1.0f / (float)a.B;
@@ -353,7 +376,7 @@ __global__ __launch_bounds__(NT) void em_grad_kernel(const StepArgs a) {
         // pred = out + obs; MSE(pred, next) over B x D; grads / (1 + tw)
         const float norm = 1.0f + a.tw;
         const float gscale = 2.0f / ((float)a.B * D) / norm;
-        float* pred = tacts[0];  // pred [D][R]: the frozen termination predictor's input
+        float* pred = lds_ptr(tacts[0]);  // pred [D][R]: the frozen termination predictor's input
         for (int t = tid; t < D * R; t += NT) {
             const float p = out[t] + x0[t];  // x0 rows k < D are the observations
             const float d = p - nobs[t];
@@ -411,6 +434,7 @@ __global__ __launch_bounds__(NT) void em_grad_kernel(const StepArgs a) {
     }
     if (N.ln_scale >= 0) {
         // g = grad wrt the LayerNorm output [K0][R]
+        g = lds_ptr(g);
         for (int k = tid; k < K0; k += NT) {
             float ss = 0.f, sb = 0.f;
             for (int r = 0; r < R; ++r) {
@@ -430,6 +454,9 @@ __global__ __launch_bounds__(NT) void em_grad_kernel(const StepArgs a) {
 // store in HBM on the way forward and come back in reverse; the gradient w.r.t. the
 // carried observation (the residual plus the LayerNorm input gradient of its D
 // features) flows from step t + 1 into step t.  Partial grads accumulate over the steps.
+#ifndef EM_SEQ_KS
+#define EM_SEQ_KS 16
+#endif
 __global__ __launch_bounds__(NT) void em_seq_grad_kernel(const StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ float lsum[NLOG][R];
@@ -514,13 +541,13 @@ __global__ __launch_bounds__(NT) void em_seq_grad_kernel(const StepArgs a) {
             const int k = q / R, r = q % R;
             const float xh = (x0[q] - mu_s[r]) * rs_s[r];
             xhat[q] = xh;
-            acts[0][q] = xh * P[N.ln_scale + k] + P[N.ln_bias + k];
+            lds_ptr(acts[0])[q] = xh * P[N.ln_scale + k] + P[N.ln_bias + k];
         }
         __syncthreads();
         for (int i = 0; i < N.n; ++i)
-            dense_fwd(P + N.w[i], P + N.b[i], acts[i], N.dims[i], N.dims[i + 1], acts[i + 1], i < N.n - 1);
-        const float* out = acts[N.n];
-        float* pred = tacts[0];
+            dense_fwd<EM_SEQ_KS>(P + N.w[i], P + N.b[i], acts[i], N.dims[i], N.dims[i + 1], acts[i + 1], i < N.n - 1);
+        const float* out = lds_ptr(acts[N.n]);
+        float* pred = lds_ptr(tacts[0]);
         for (int q = tid; q < D * R; q += NT) {
             const float p = out[q] + x0[q];
             const float d = p - nobs[q];
@@ -529,13 +556,13 @@ __global__ __launch_bounds__(NT) void em_seq_grad_kernel(const StepArgs a) {
             atomicAdd(&lsum[0][q % R], d * d);
         }
         __syncthreads();
-        if (a.tw > 0.f) tp_score(a, tacts, gA, gB, gC, lab, lsum, inv_n, norm);
+        if (a.tw > 0.f) tp_score<EM_SEQ_KS>(a, tacts, gA, gB, gC, lab, lsum, inv_n, norm);
         if (a.train) {
             float* st = sq + (long long)t * a.seq_stride;
             for (int q = tid; q < K0 * R; q += NT) st[q] = xhat[q];
             if (tid < R) st[K0 * R + tid] = rs_s[tid];
             float* sa = st + K0 * R + R;
-            for (int q = tid; q < act_floats; q += NT) sa[q] = acts[0][q];  // acts[0..n-1] are contiguous
+            for (int q = tid; q < act_floats; q += NT) sa[q] = lds_ptr(acts[0])[q];  // acts[0..n-1] are contiguous
             float* sg = sa + act_floats;
             for (int q = tid; q < D * R; q += NT) sg[q] = gA[q];
         }
@@ -557,7 +584,7 @@ __global__ __launch_bounds__(NT) void em_seq_grad_kernel(const StepArgs a) {
         for (int q = tid; q < K0 * R; q += NT) xhat[q] = st[q];
         if (tid < R) rs_s[tid] = st[K0 * R + tid];
         const float* sa = st + K0 * R + R;
-        for (int q = tid; q < act_floats; q += NT) acts[0][q] = sa[q];
+        for (int q = tid; q < act_floats; q += NT) lds_ptr(acts[0])[q] = sa[q];
         const float* sg = sa + act_floats;
         // total gradient w.r.t. this step's prediction: its own loss terms + the next step's
         for (int q = tid; q < D * R; q += NT) {
@@ -570,12 +597,13 @@ __global__ __launch_bounds__(NT) void em_seq_grad_kernel(const StepArgs a) {
         float* gn = gB;
         for (int i = N.n - 1; i >= 0; --i) {
             dense_dw(acts[i], g, N.dims[i], N.dims[i + 1], pg + N.w[i], pg + N.b[i], acc);
-            dense_dx(a.wt + N.w[i], g, N.dims[i], N.dims[i + 1], gn, i > 0 ? acts[i] : nullptr);
+            dense_dx<EM_SEQ_KS>(a.wt + N.w[i], g, N.dims[i], N.dims[i + 1], gn, i > 0 ? acts[i] : nullptr);
             float* tmp = g;
             g = gn;
             gn = tmp;
         }
         // g = grad w.r.t. the LayerNorm output [K0][R]
+        g = lds_ptr(g);
         for (int k = tid; k < K0; k += NT) {
             float ss = 0.f, sb = 0.f;
             for (int r = 0; r < R; ++r) {
