@@ -581,11 +581,26 @@ __global__ __launch_bounds__(NT) void em_seq_grad_kernel(const StepArgs a) {
     for (int t = T - 1; t >= 0; --t) {
         const bool acc = t < T - 1;
         const float* st = sq + (long long)t * a.seq_stride;
-        for (int q = tid; q < K0 * R; q += NT) xhat[q] = st[q];
-        if (tid < R) rs_s[tid] = st[K0 * R + tid];
-        const float* sa = st + K0 * R + R;
-        for (int q = tid; q < act_floats; q += NT) lds_ptr(acts[0])[q] = sa[q];
-        const float* sg = sa + act_floats;
+        {
+            // the step's record (xhat | rstd | acts[0..n-1]) in batches of 8 loads per thread,
+            // all in flight before their LDS stores (one HBM round trip per element otherwise)
+            constexpr int BQ = 8;
+            const int n1 = K0 * R, n2 = n1 + R, n3 = n2 + act_floats;
+            float* const a0 = lds_ptr(acts[0]);
+            for (int q0 = tid; q0 < n3; q0 += BQ * NT) {
+                float v[BQ];
+#pragma unroll
+                for (int j = 0; j < BQ; ++j) v[j] = st[min(q0 + j * NT, n3 - 1)];  // unguarded
+#pragma unroll
+                for (int j = 0; j < BQ; ++j) {
+                    const int q = q0 + j * NT;
+                    if (q < n1) xhat[q] = v[j];
+                    else if (q < n2) rs_s[q - n1] = v[j];
+                    else if (q < n3) a0[q - n2] = v[j];
+                }
+            }
+        }
+        const float* sg = st + K0 * R + R + act_floats;
         // total gradient w.r.t. this step's prediction: its own loss terms + the next step's
         for (int q = tid; q < D * R; q += NT) {
             const float gv = sg[q] + (acc ? carry[q] : 0.f);
