@@ -345,7 +345,17 @@ def main(argv=None):
     torch.cuda.set_device(dev_index)
     if distributed:
         if args.share_device:
-            dist.init_process_group("gloo")
+            # gloo's rendezvous prints "[Gloo] Rank r is connected to ..." on stdout, which
+            # carries only the JSON line: point fd 1 at stderr while it connects
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo")
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
 

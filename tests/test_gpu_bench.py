@@ -54,8 +54,8 @@ def test_bench_self_launches_ranks_sharing_the_device():
                 "--no-cpu-baseline", "--eval-envs", "0", "--envmodel-train-steps", "0", "--kernel-iters", "2",
                 "--preheat-ms", "20", "--members", "4"])
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]  # stdout: the JSON line only
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["share_device"] is True
     assert d["config"]["global_batch"] == 256 * 4 * 2
