@@ -10,6 +10,16 @@
 //   critic_loss / actor_loss (fql/agents/fql.py) -> loss_* kernels
 //   jax.grad                           -> bwd_* kernels + gemm_kernel (dX, dW layouts)
 //   optax.adam + target_update         -> adam_kernel ; apply_loss_fn grad stats -> finalize_kernel
+//
+// The production step (H = 512) runs the fused forms: stream_fwd_kernel (whole-network
+// forwards), euler_flow_kernel (Euler steps 1..9 in one persistent launch),
+// stream_bwd_kernel (whole dX chains), gemm_group_kernel_o4<..., EPI_ADAM> (every dW of a net
+// with optax.adam / the target EMA / W^T copies / grad stats in the epilogue); the per-layer
+// kernels above remain the path for other widths (engine options select either).
+//
+// Sections: GEMM and the fused optimiser epilogue | persistent Euler flow | column
+// reductions | LayerNorm | head | streamed forward | backward | streamed backward | RNG |
+// sampling | losses | optimiser | init | world-model rollout.
 #include "kernels.h"
 
 #include <hip/hip_runtime.h>
