@@ -302,6 +302,9 @@ def main(argv=None):
                          "(csrc/tools/pmc_summary.py output); missing file -> traffic null")
     ap.add_argument("--preheat-ms", type=float, default=300.0,
                     help="replays of the dominant kernel alone before the warmup steps (GPU clock ramp); 0 = off")
+    ap.add_argument("--preheat-kind", choices=("steps", "kernel"), default="steps",
+                    help="steps: population steps of a second, throwaway population on the same device "
+                         "(the timed population is untouched); kernel: replays of the dominant kernel alone")
     ap.add_argument("--no-probe", action="store_true",
                     help="time the step without the in-step timing nodes of the dominant kernel")
     ap.add_argument("--eval-envs", type=int, default=50, help="world-model rollout leg: envs per member "
@@ -385,6 +388,12 @@ def main(argv=None):
                             use_graph=not args.no_graph)
     pop = Population(pcfg, alphas, seeds, device=dev_index)
     pop.set_dataset(dev_data)
+    scratch = None
+    if args.preheat_ms > 0 and args.preheat_kind == "steps":
+        # a second population of the same shape (own parameters, optimiser state and dataset
+        # copy): its steps warm the GPU; the timed population's state is never touched by them
+        scratch = Population(pcfg, alphas, seeds, device=dev_index)
+        scratch.set_dataset(dev_data)
     del dev_data
     torch.cuda.empty_cache()
 
@@ -399,11 +408,20 @@ def main(argv=None):
     # Replays of the dominant kernel alone (not steps; results discarded) bring it
     # there before the warmup steps, so a short --steps/--warmup run measures the
     # steady-state step, not the clock ramp.
-    preheat_ms = 0.0
+    # The kernel replays still left a ramp that only the step's own mix of MFMA, L2 and HBM
+    # work warms: the default preheat therefore steps a throwaway population
+    # (same shapes and schedule) instead, and the W warmup steps of the timed population follow.
+    preheat_ms, preheat_steps = 0.0, 0
     if args.preheat_ms > 0:
         t_ph = time.perf_counter()
-        iso_us0, _ = pop.time_dominant_kernel(1)
-        pop.time_dominant_kernel(max(1, int(args.preheat_ms * 1e3 / max(iso_us0, 1.0))))
+        if scratch is not None:
+            while 1e3 * (time.perf_counter() - t_ph) < args.preheat_ms:
+                scratch.step(10)
+                scratch.sync()
+                preheat_steps += 10
+        else:
+            iso_us0, _ = pop.time_dominant_kernel(1)
+            pop.time_dominant_kernel(max(1, int(args.preheat_ms * 1e3 / max(iso_us0, 1.0))))
         torch.cuda.synchronize()
         preheat_ms = 1e3 * (time.perf_counter() - t_ph)
     pop.set_probe(not args.no_probe)
@@ -508,10 +526,16 @@ def main(argv=None):
             "traffic": traffic,
         },
         "cpu_baseline": None,
-        "preheat": {"ms": round(preheat_ms, 1),
-                    "what": "replays of the dominant kernel alone (no steps, results discarded) before the "
-                            "warmup steps, so the timed steps run at the steady GPU clock"},
+        "preheat": {"ms": round(preheat_ms, 1), "kind": args.preheat_kind if args.preheat_ms > 0 else None,
+                    "steps": preheat_steps,
+                    "what": ("population steps of a second, throwaway population of the same shape (own "
+                             "parameters, optimiser state and dataset copy; the timed population is not "
+                             "stepped by it)" if args.preheat_kind == "steps" else
+                             "replays of the dominant kernel alone (no steps, results discarded)")
+                            + " before the warmup steps, so the timed steps run at the steady GPU clock"},
     }
+    if scratch is not None:
+        scratch.close()
     if args.eval_envs > 0:
         result["eval_rollout"] = eval_rollout_leg(pop, wl, args.eval_envs, args.eval_steps, dev)
     if args.envmodel_train_steps > 0 and rank == 0:
