@@ -300,6 +300,8 @@ struct SampleArgs {
     const float* inj_noise;
     const uint64_t* seeds;    // per slot
     const int* count;         // per slot (Adam count == update index)
+    int step_add;             // added to count (cross-step groups: a snapshot of count at the group's
+                              // start + the step's position in the group)
     unsigned stream_salt;     // distinguishes train / val draws
     int B, D, A;
     // outputs (feature-major)

@@ -2349,7 +2349,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const SampleArgs a) {
     if (b >= a.B) return;
     const int B = a.B, D = a.D, A = a.A;
     const uint64_t seed = a.seeds[slot];
-    const uint32_t step = (uint32_t)a.count[slot];
+    const uint32_t step = (uint32_t)(a.count[slot] + a.step_add);
     const long long B2 = 2 * (long long)B, B3 = 3 * (long long)B;
     float* os = at(a.os_in, slot);
     float* bc = at(a.bc_in, slot);

@@ -19,6 +19,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <vector>
@@ -78,6 +79,8 @@ struct EngineOptions {
     int dw_tile_critic = 10, dw_tile_actor = 10;  // grouped dW tile ids (launch_gemm_group_dw)
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
     int dw_stagger = 0;    // fused dW + optimiser: first-wave start offsets (AdamEpi::stagger)
+    int xstep = 0;         // 1: each step's critic dW / optimiser + finalize at the head of the next
+                           // step's graph (inside one fqlpop_step call; fqlpop::xstep)
 };
 EngineOptions g_engine_opts;
 
@@ -95,6 +98,7 @@ const EngineOptionRef kEngineOptions[] = {
     {"dw_tile_actor", &EngineOptions::dw_tile_actor, 0, 10},
     {"adam_nt", &EngineOptions::adam_nt, 0, 3},
     {"dw_stagger", &EngineOptions::dw_stagger, 0, 256},
+    {"xstep", &EngineOptions::xstep, 0, 1},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -230,6 +234,7 @@ struct fqlpop {
     // activations (slot-strided)
     std::vector<float*> allocs;
     float *os_in, *bc_in, *eu_in, *cr_in, *tg_in;
+    float* cr_in_buf[2] = {nullptr, nullptr};  // cr_in per parameter buffer (cr_in = cr_in_buf[cur])
     std::vector<float*> os_u, os_g, bc_u, bc_g, eu_g, cr_u, cr_h, cr_mu, cr_rs, tg_u, tg_h, tg_mu, tg_rs;
     std::vector<float*> cr_du, bc_du, os_du;
     float *cr_dh, *bc_dh, *os_dh, *cr_c1, *cr_c2;
@@ -240,6 +245,19 @@ struct fqlpop {
 
     hipStream_t sM = nullptr, sF = nullptr, sB = nullptr, sX = nullptr;
     hipEvent_t ev_sample, ev_bcfwd, ev_bcloss, ev_flow, ev_bdone, ev_t0, ev_t1;
+    // cross-step critic tail (engine option xstep): inside one fqlpop_step call, every step but
+    // the last leaves its critic partial fold + fused dW / optimiser and the grad-stat finalize
+    // out of its graph (xs_out); the next step's graph runs them on sB at its head (xs_in),
+    // beside its sampling, one-step and BC forwards and flow, and its target-critic and critic
+    // forwards wait for them (ev_cdone).  The sampler of an xs_in step reads count + 1 before
+    // that finalize increments count (finalize waits for the sampler).  cr_in alternates with
+    // the parameter buffer, so the next sampler never writes the dW's layer-0 operand.
+    bool xstep = false;
+    bool xs_in = false, xs_out = false;    // flags of the step being enqueued
+    bool skip_dw_wait = false;             // the deferred dW half runs in the next graph
+    std::function<void()> xs_tail[2];      // deferred critic dW half, per parameter buffer
+    std::set<long long> xs_built;          // (active count, probe set) with every variant captured
+    hipEvent_t ev_cdone = nullptr;
     std::vector<hipEvent_t> ev_pool;
     int ev_next = 0;
     // in-step timing probe of the dominant kernel (Euler hidden-layer GEMM):
@@ -725,7 +743,7 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
     // captured ahead of it
     const int NP = a.NP;
     auto dw_half = [=, &N]() {
-    if (ev) HIPCHK(hipStreamWaitEvent(sw, ev, 0));
+    if (ev && !h->skip_dw_wait) HIPCHK(hipStreamWaitEvent(sw, ev, 0));
     ColsumArgs r{};
     r.part = part; r.NP = NP; r.tiles = Mg / 16;
     r.grads = h->grads + N.off; r.P = h->P; r.ens = N.ens_size;
@@ -1014,6 +1032,8 @@ void euler_phase_report(const unsigned long long* ph, long long nb, int L, int s
     std::fprintf(stderr, "  head per step: %.3f\n", kl[L] * per);
 }
 
+void flip_params(fqlpop* h);
+
 // Enqueue one population update (train) or one total_loss pass (!train).
 void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     const Ctx c{h, h->nz};
@@ -1023,6 +1043,24 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     hipStream_t sM = h->sM, sF = h->sF, sB = h->sB, sX = h->sX;
     h->ev_next = 0;
     h->probe_idx = 0;
+    h->cr_in = h->cr_in_buf[h->cur];
+    const bool xin = train && h->xs_in, xout = train && h->xs_out;  // cross-step critic tail (fqlpop::xstep)
+    if (xin) {
+        // the previous step's critic partial fold + fused dW / optimiser on sB, with that step's
+        // parameter buffers (its closure reads them from h): first in the graph, no wait (the
+        // previous graph, which produced its operands, has completed)
+        ARGCHK(h->xs_tail[h->cur ^ 1], "cross-step tail: no deferred critic optimiser");
+        // sB joins the capture first (a launch on a stream outside the capture would run
+        // eagerly instead of becoming a node of this graph)
+        HIPCHK(hipEventRecord(h->ev_cdone, sM));
+        HIPCHK(hipStreamWaitEvent(sB, h->ev_cdone, 0));
+        flip_params(h);
+        h->skip_dw_wait = true;
+        h->xs_tail[h->cur]();
+        h->skip_dw_wait = false;
+        flip_params(h);
+        h->cr_in = h->cr_in_buf[h->cur];
+    }
     // the persistent Euler launch writes both stamps of every block it launches, and the
     // reduction reads only those (probe_nz): no per-step clearing node at the step's head
     if (h->probe_set >= 0 && !h->euler_fused)
@@ -1037,6 +1075,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     sa.inj_batch = inj_batch ? h->inj_batch : nullptr;
     sa.inj_noise = inj_noise ? h->inj_noise : nullptr;
     sa.seeds = h->skeys; sa.count = h->count;
+    sa.step_add = xin ? 1 : 0;  // count is the previous step's until its finalize below
     sa.stream_salt = train ? 0x51A7u : 0x5A1Du;
     sa.B = B; sa.D = D; sa.A = A;
     sa.os_in = tref(h->os_in, (long long)Kc * B3);
@@ -1063,6 +1102,18 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         HIPCHK(hipEventRecord(h->ev_sample, sM));
         HIPCHK(hipStreamWaitEvent(sF, h->ev_sample, 0));
         HIPCHK(hipStreamWaitEvent(sB, h->ev_sample, 0));
+    }
+    if (xin) {
+        // the previous step's finalize (grad stats, count += 1) after its critic optimiser and
+        // after this step's sampler read count
+        FinalArgs fa{};
+        fa.stats = h->stats; fa.chunk_leaf = h->chunk_leaf; fa.leaf_first = h->leaf_first;
+        fa.n_total_chunks = h->n_chunks_total; fa.n_leaves = h->n_train_leaves;
+        fa.info = tref(h->info, FQLPOP_INFO_STRIDE);
+        fa.count = h->count;
+        fa.nz = c.nz; fa.slots = h->slots;
+        launch_finalize(fa, sB);
+        HIPCHK(hipEventRecord(h->ev_cdone, sB));
     }
 
     float* info = train ? h->info : h->vinfo;
@@ -1176,6 +1227,9 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         }
     }
     dep(sM, sX);  // a' is in the target-critic input
+    // cross-step tail: the previous step's critic optimiser (target EMA, critic params and
+    // W^T) and finalize (count) are done before this step's target critic and critic read them
+    if (xin) HIPCHK(hipStreamWaitEvent(sX, h->ev_cdone, 0));
     const NetLayout& NC = h->critic;
     const long long sy2 = (long long)H * B2, sy1 = (long long)H * B;
     // ---- sX: target critic on [s', a'] (params from the target arena) -----
@@ -1219,6 +1273,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         launch_head_fwd(HEAD_STORE, ht, sX);
     }
     // ---- sM: critic on [s,a ; s,clip(a_pi)] -------------------------------
+    if (xin && sX != sM) HIPCHK(hipStreamWaitEvent(sM, h->ev_cdone, 0));
     {
         const NetLayout& N = NC;
         HeadArgs hc = head_args(c, N, h->cr_h[L - 1], B2, B2, sy2);
@@ -1282,8 +1337,16 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3,
                            B, B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, B, h->part_os, sM, nullptr,
                            &os_dw);
-            critic_dw();  // the fused launches include each net's small-leaf Adam
+            if (xout) h->xs_tail[h->cur] = critic_dw;  // (the next step's graph runs it)
+            else critic_dw();  // the fused launches include each net's small-leaf Adam
             os_dw();
+            if (xout) {
+                // this step's finalize runs in the next step's graph too: join the streams
+                dep(sB, sM);
+                HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
+                HIPCHK(hipGetLastError());
+                return;
+            }
             if (h->cdw_sb) dep(sB, sM);
         } else if (h->stream_bwd)
             stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3,
@@ -1320,6 +1383,8 @@ void flip_params(fqlpop* h) {
     h->paramsT_nx = h->paramsT_buf[h->cur ^ 1];
 }
 
+Graphs& graph_for(fqlpop* h, bool train, bool inj_batch, bool inj_noise, bool recapture);
+
 void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     if (h->nz == 0) return;
     if (h->stream_bwd && h->wt_dirty) {  // params set on the host side since the last step
@@ -1332,12 +1397,21 @@ void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         if (train) flip_params(h);
         return;
     }
+    Graphs& gr = graph_for(h, train, inj_batch, inj_noise, false);
+    HIPCHK(hipGraphLaunch(gr.exec, h->sM));
+    if (train) flip_params(h);
+}
+
+// The graph of one step for the current (mode, active count, probe set, parameter buffer,
+// cross-step flags), captured if missing (or always, with `recapture`).
+Graphs& graph_for(fqlpop* h, bool train, bool inj_batch, bool inj_noise, bool recapture) {
     // one graph per (mode, active-member count): kernels read the active slot ids
     // from device memory, so any active set of the same size replays the graph
     const long long key = ((train ? 4 : 0) + (inj_batch ? 2 : 0) + (inj_noise ? 1 : 0)) + 8LL * h->nz +
-                          (1LL << 32) * (h->probe_set + 1) + (1LL << 36) * h->cur;
+                          (1LL << 32) * (h->probe_set + 1) + (1LL << 36) * h->cur +
+                          (1LL << 38) * ((h->xs_in ? 1 : 0) + (h->xs_out ? 2 : 0));
     Graphs& gr = h->graphs[key];
-    if (gr.exec == nullptr || gr.nz != h->nz) {
+    if (recapture || gr.exec == nullptr || gr.nz != h->nz) {
         if (gr.exec) HIPCHK(hipGraphExecDestroy(gr.exec));
         gr.exec = nullptr;
         hipGraph_t graph;
@@ -1354,9 +1428,37 @@ void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         HIPCHK(hipGraphDestroy(graph));
         gr.nz = h->nz;
     }
-    HIPCHK(hipGraphLaunch(gr.exec, h->sM));
-    if (train) flip_params(h);
+    return gr;
 }
+
+// Cross-step tail (fqlpop::xstep): capture every step graph variant a multi-step
+// fqlpop_step call uses, for both parameter buffers and (probe on) both probe sets, in an
+// order where each xs_in capture finds the deferred critic dW half of the other buffer's
+// xs_out capture of the same active count.  Once per active count (and after a parameter
+// upload); so that no graph is captured inside a caller's timed loop.
+void xs_prebuild(fqlpop* h) {
+    const long long tag = (long long)h->nz * 2 + (h->probe_set >= 0 ? 1 : 0);  // (both probe sets)
+    if (h->xs_built.count(tag)) return;
+    const int set0 = h->probe_set, cur0 = h->cur;
+    const bool in0 = h->xs_in, out0 = h->xs_out;
+    // (parity offset from cur0, xs_in, xs_out)
+    const int order[8][3] = {{0, 0, 1}, {1, 1, 1}, {0, 1, 1}, {1, 0, 1}, {0, 1, 0}, {1, 1, 0}, {0, 0, 0}, {1, 0, 0}};
+    for (int ps = 0; ps < (set0 >= 0 ? 2 : 1); ++ps) {
+        h->probe_set = set0 >= 0 ? set0 ^ ps : -1;
+        for (const auto& o : order) {
+            if ((h->cur ^ cur0) != o[0]) flip_params(h);
+            h->xs_in = o[1] != 0;
+            h->xs_out = o[2] != 0;
+            (void)graph_for(h, true, false, false, true);
+        }
+    }
+    if (h->cur != cur0) flip_params(h);
+    h->probe_set = set0;
+    h->xs_in = in0;
+    h->xs_out = out0;
+    h->xs_built.insert(tag);
+}
+
 
 // Launch duration from per-block stamps: max(end) - min(start) over the blocks
 // that ran (0 = slot not written).  s_memrealtime counts at 100 MHz.
@@ -1548,6 +1650,10 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         h->cdw_sb = eo.cdw_sb != 0;
         // Adam / EMA / W^T / grad stats fused into the grouped dW epilogue
         h->fused_adam = h->stream_bwd && H % 128 == 0 && L <= GEMM_GROUP_MAX && h->critic.off == 0 && eo.fused_adam;
+        // cross-step critic tail: the graph path of the default schedule only (fused Euler,
+        // streamed backward, fused optimiser with the critic's on sB, three streams)
+        h->xstep = eo.xstep != 0 && cfg->use_graph && h->euler_fused && h->stream_bwd && h->fused_adam &&
+                   h->cdw_sb && eo.streams == 3 && !eo.serial;
         if (h->euler_fused) {  // dominant kernel: one persistent Euler launch per step
             h->probe_pairs = 1;
             h->probe_blocks = (long long)(cfg->batch_size / 16) * n_members;
@@ -1581,7 +1687,7 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         for (auto& e : h->probe_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHK(hipStreamCreateWithFlags(&h->probe_stream, hipStreamNonBlocking));
         for (auto& e : h->ev_pool) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        for (hipEvent_t* e : {&h->ev_sample, &h->ev_bcfwd, &h->ev_bcloss, &h->ev_flow, &h->ev_bdone})
+        for (hipEvent_t* e : {&h->ev_sample, &h->ev_bcfwd, &h->ev_bcloss, &h->ev_flow, &h->ev_bdone, &h->ev_cdone})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         HIPCHK(hipEventCreate(&h->ev_t0));
         HIPCHK(hipEventCreate(&h->ev_t1));
@@ -1609,7 +1715,8 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         h->os_in = h->alloc(align_up((long long)Kc * B3));
         h->bc_in = h->alloc(align_up((long long)Kb * B2));
         h->eu_in = h->alloc(align_up((long long)Kb * B));
-        h->cr_in = h->alloc(align_up((long long)Kc * B2));
+        for (float*& cb : h->cr_in_buf) cb = h->alloc(align_up((long long)Kc * B2));
+        h->cr_in = h->cr_in_buf[0];
         h->tg_in = h->alloc(align_up((long long)Kc * B));
         for (int l = 0; l < L; ++l) {
             h->os_u.push_back(h->alloc((long long)H * B3));
@@ -1691,7 +1798,7 @@ int fqlpop_destroy(fqlpop_t* h) {
         for (auto& d : h->ds)
             for (float* p : {d.obs, d.act, d.rew, d.mask, d.nobs})
                 if (p) (void)hipFree(p);
-        for (hipEvent_t e : {h->ev_sample, h->ev_bcfwd, h->ev_bcloss, h->ev_flow, h->ev_bdone, h->ev_t0, h->ev_t1})
+        for (hipEvent_t e : {h->ev_sample, h->ev_bcfwd, h->ev_bcloss, h->ev_flow, h->ev_bdone, h->ev_cdone, h->ev_t0, h->ev_t1})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
         for (hipEvent_t e : h->probe_done)
@@ -1749,6 +1856,7 @@ int fqlpop_set_dataset(fqlpop_t* h, int which, const float* obs, const float* ac
         // graphs bake dataset pointers in: drop them
         for (auto& kv : h->graphs)
             if (kv.second.exec) { HIPCHK(hipGraphExecDestroy(kv.second.exec)); kv.second.exec = nullptr; }
+        h->xs_built.clear();
     });
 }
 
@@ -1771,18 +1879,28 @@ int fqlpop_step(fqlpop_t* h, int n_steps) {
         ARGCHK(n_steps >= 0, "n_steps must be >= 0");
         if (h->ds[0].rows == 0) throw FqErr{FQLPOP_E_STATE, "no training dataset set (fqlpop_set_dataset)"};
         HIPCHK(hipSetDevice(h->device));
+        struct XsReset {  // (also on an exception)
+            fqlpop* h;
+            ~XsReset() { h->xs_in = h->xs_out = false; }
+        } xs_reset{h};
+        const bool xs = h->xstep && n_steps >= 2 && h->nz > 0;
         for (int i = 0; i < n_steps; ++i) {
+            // cross-step tail: every step but the last defers its critic optimiser to the next
+            h->xs_in = xs && i > 0;
+            h->xs_out = xs && i < n_steps - 1;
             if (h->probe) {
                 const int set = (int)(h->probe_step & 1);
                 if (h->probe_pending[set]) probe_consume(h, set);  // the step i-2 that used this set
                 h->probe_set = set;
                 h->probe_nz[set] = h->nz;
+                if (xs) xs_prebuild(h);
                 run(h, true, false, false);
                 h->probe_set = -1;
                 HIPCHK(hipEventRecord(h->probe_done[set], h->sM));
                 h->probe_pending[set] = true;
                 ++h->probe_step;
             } else {
+                if (xs) xs_prebuild(h);
                 run(h, true, false, false);
             }
         }

@@ -314,7 +314,7 @@ def _sampled_run(H, B, steps, opts):
         return _sampled_run_now(H, B, steps)
 
 
-def _sampled_run_now(H, B, steps):
+def _sampled_run_now(H, B, steps, calls=None, probe=False):
     rng = np.random.default_rng(7)
     N = 4000
     obs = rng.standard_normal((N, 28)).astype(np.float32)
@@ -324,8 +324,13 @@ def _sampled_run_now(H, B, steps):
             "next_observations": (obs + 0.05 * rng.standard_normal((N, 28))).astype(np.float32)}
     pop = _pop(H, B, [3.0, 30.0, 300.0], [5, 6, 7])
     pop.set_dataset(data)
-    pop.step(steps)
+    if probe:
+        pop.set_probe(True)
+    for n in calls or [steps]:
+        pop.step(n)
     out = (pop.read_info_array().copy(), [pop.get_flat(i, w) for i in range(3) for w in (0, 1, 2)])
+    if probe:
+        out = out + (pop.read_probe(), [pop.get_count(i) for i in range(3)])
     pop.close()
     return out
 
@@ -426,3 +431,22 @@ def test_device_init_properties():
         assert pop.get_count(i) == 0
         assert not np.any(pop.get_flat(i, STATE_ADAM_M)) and not np.any(pop.get_flat(i, STATE_ADAM_V))
     pop.close()
+
+
+@pytest.mark.parametrize("calls", [[7], [5, 1, 9, 2]])
+def test_cross_step_tail_bit_identical(calls):
+    """Engine option xstep: inside one step() call every step's critic dW / optimiser and
+    grad-stat finalize run at the head of the next step's graph (sampler reads count + 1
+    ahead of that finalize; cr_in per parameter buffer).  Several calls, one of a single
+    step, give the same parameters, Adam state, target, info and counts as the default
+    schedule, and the in-step probe times every step's Euler launch once."""
+    steps = sum(calls)
+    with engine_options():
+        ref = _sampled_run_now(512, 256, steps, calls, probe=True)
+    with engine_options(xstep=1):
+        got = _sampled_run_now(512, 256, steps, calls, probe=True)
+    assert np.array_equal(got[0], ref[0])
+    for a, b in zip(got[1], ref[1]):
+        assert np.array_equal(a, b)
+    assert got[3] == ref[3] == [steps] * 3
+    assert got[2][1] == ref[2][1] == steps, (got[2], ref[2])
