@@ -79,6 +79,7 @@ struct EngineOptions {
     int dw_tile_critic = 10, dw_tile_actor = 10;  // grouped dW tile ids (launch_gemm_group_dw)
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
     int dw_stagger = 0;    // fused dW + optimiser: first-wave start offsets (AdamEpi::stagger)
+    int bc_late = 0;       // BC loss / backward / optimiser after the critic forward (1) or backward (2)
     int xstep = 0;         // 1: each step's critic dW / optimiser + finalize at the head of the next
                            // step's graph (inside one fqlpop_step call; fqlpop::xstep)
 };
@@ -99,6 +100,7 @@ const EngineOptionRef kEngineOptions[] = {
     {"adam_nt", &EngineOptions::adam_nt, 0, 3},
     {"dw_stagger", &EngineOptions::dw_stagger, 0, 256},
     {"xstep", &EngineOptions::xstep, 0, 1},
+    {"bc_late", &EngineOptions::bc_late, 0, 2},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -1189,7 +1191,10 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     };
 
     // ---- sB: BC loss + backward + Adam ------------------------------------
-    // (Adam writes params_nx, so it need not wait for the flow's reads)
+    // (Adam writes params_nx, so it need not wait for the flow's reads).  Engine option
+    // bc_late: captured after the critic forward (1) or backward (2) of the main chain, whose
+    // completion it then waits for (schedule experiment)
+    auto bc_chain = [&]() {
     HIPCHK(hipStreamWaitEvent(sB, h->ev_bcfwd, 0));
     launch_loss_bc(la, sB);
     HIPCHK(hipEventRecord(h->ev_bcloss, sB));
@@ -1207,6 +1212,8 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         }
     }
     HIPCHK(hipEventRecord(h->ev_bdone, sB));
+    };
+    if (h->opt.bc_late == 0) bc_chain();
 
     // ---- sM: one-step actor forward on [s'; s; s] (z_next; z_d; z_metric) --
     {
@@ -1291,6 +1298,10 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         }
     }
     dep(sX, sM);  // Q_target
+    if (h->opt.bc_late == 1) {
+        dep(sM, sB);
+        bc_chain();
+    }
     launch_loss_critic(la, sM);
     // fused optimiser: the critic's dW + Adam is captured after the actor's dX
     // chain (it runs beside it instead of ahead of it on a shared queue)
@@ -1319,6 +1330,10 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             adam_net(c, sX, 0);
             if (h->stream_bwd) transpose_nets(h, sX, 1, false, h->params_nx, h->paramsT_nx);
         }
+    }
+    if (h->opt.bc_late == 2) {
+        dep(sM, sB);
+        bc_chain();
     }
     HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
     HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));

@@ -81,7 +81,8 @@ const char* fqlpop_last_error(void);
  *   streams (3/4), prio (0..2), dw_tile_critic / dw_tile_actor (0..10), adam_nt (0..3),
  *   dw_stagger (0..256: start offsets of the fused dW + optimiser launch's first blocks),
  *   xstep (0/1: inside one fqlpop_step call, each step's critic dW / optimiser runs at the
- *   head of the next step's graph, beside its sampling and actor forwards).
+ *   head of the next step's graph, beside its sampling and actor forwards),
+ *   bc_late (0..2: the BC update after the critic forward / backward of the main chain).
  * The defaults are the measured-fastest configuration.  Unknown names or values
  * out of range: FQLPOP_E_ARG.  The production library reads no environment
  * variable; result-changing timing switches exist only in diagnostic builds. */
