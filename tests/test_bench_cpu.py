@@ -50,3 +50,20 @@ def test_engine_options_validate_and_reset():
         fqlpop.set_engine_option("no_such_option", 1)
     with pytest.raises(fqlpop.FqlpopError):
         fqlpop.set_engine_option("streams", 7)
+
+
+def test_schedule_experiment_options_default_off():
+    """The schedule experiments measured slower stay off by default and
+    are range-checked: xstep (critic optimiser at the head of the next step's graph) 0..1,
+    bc_late (BC update after the critic forward / backward) 0..2."""
+    import pytest
+    import fqlpop
+    fqlpop.reset_engine_options()
+    assert fqlpop.get_engine_option("xstep") == 0
+    assert fqlpop.get_engine_option("bc_late") == 0
+    for name, hi in (("xstep", 1), ("bc_late", 2)):
+        fqlpop.set_engine_option(name, hi)
+        assert fqlpop.get_engine_option(name) == hi
+        with pytest.raises(fqlpop.FqlpopError):
+            fqlpop.set_engine_option(name, hi + 1)
+    fqlpop.reset_engine_options()

@@ -450,3 +450,14 @@ def test_cross_step_tail_bit_identical(calls):
         assert np.array_equal(a, b)
     assert got[3] == ref[3] == [steps] * 3
     assert got[2][1] == ref[2][1] == steps, (got[2], ref[2])
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_bc_late_schedule_bit_identical(mode):
+    """Engine option bc_late (the BC update captured after the critic forward / backward) only
+    moves launches in the step's DAG: the same parameters, Adam state, target and info."""
+    ref = _sampled_run(512, 256, 3, {})
+    got = _sampled_run(512, 256, 3, {"bc_late": mode})
+    assert np.array_equal(got[0], ref[0])
+    for a, b in zip(got[1], ref[1]):
+        assert np.array_equal(a, b)
