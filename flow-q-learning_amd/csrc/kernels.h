@@ -156,6 +156,12 @@ struct HeadArgs {         // out'[j][m] = sum_k W[k][j] h'[k][m] + b[j]
     float t_next;         // HEAD_EULER/BC_FUSED: time row value of the next step
     int ny, nz;
     const int* slots;
+    // HEAD_STORE of the critic forward with the critic-loss gradient seeds fused (dq.p set;
+    // nout 1, M = 2B, y = ensemble member): dq[y][m] = 2 (Q - target) / (E B) for the
+    // (s, a) columns m < B, gpi for the (s, a_pi) columns (loss_critic_kernel's values)
+    TRef dq, qt, rew, mask;
+    float discount, inv_eb, gpi;
+    int q_min, E;
 };
 void launch_head_fwd(int mode, const HeadArgs& a, hipStream_t s);
 
@@ -330,6 +336,7 @@ struct LossArgs {
     int B, A, E, da_n;
     int q_min, normq;
     float discount;
+    int dq_fused;                 // loss_critic: dq already written by the critic forward's head
     int nz;
     const int* slots;
 };

@@ -1320,6 +1320,23 @@ DEV void head_write(const HeadArgs& a, int slot, int y, int j, int m, float v) {
     const int B = a.B, D = a.D;
     if constexpr (MODE == HEAD_STORE) {
         at(a.o0, slot, y)[(long long)j * a.ld0 + m] = v;
+        if (a.dq.p != nullptr) {
+            // the critic-loss gradient seed of this Q, as loss_critic_kernel computes it
+            float g = a.gpi;
+            if (m < B) {
+                const float* qt = at(a.qt, slot);
+                float agg = a.q_min ? INFINITY : 0.f;
+                for (int e = 0; e < a.E; ++e) {
+                    const float u = qt[e * a.qt.sy + m];
+                    agg = a.q_min ? fminf(agg, u) : agg + u;
+                }
+                if (!a.q_min) agg /= (float)a.E;
+                const float yv = at(a.rew, slot)[m] + a.discount * at(a.mask, slot)[m] * agg;
+                const float d = v - yv;
+                g = 2.0f * d * a.inv_eb;
+            }
+            at(a.dq, slot, y)[m] = g;
+        }
     } else if constexpr (MODE == HEAD_ACT) {
         at(a.o0, slot, y)[(long long)j * a.ld0 + m] = clip1(v);
     } else if constexpr (MODE == HEAD_BC_FUSED) {
@@ -2496,7 +2513,7 @@ __global__ __launch_bounds__(256) void loss_critic_kernel(const LossArgs a) {
             qmx = fmaxf(qmx, qv);
             qmn = fminf(qmn, qv);
             const float g = 2.0f * d * invEB;
-            dq[e * a.dq.sy + b] = g;
+            if (!a.dq_fused) dq[e * a.dq.sy + b] = g;
             if (e < 4) sdq[e] += g;
             qp += q[e * a.q.sy + B + b];
         }
@@ -2526,8 +2543,9 @@ __global__ __launch_bounds__(256) void loss_critic_kernel(const LossArgs a) {
     const float qmean_pi = qpi_s / (float)B;
     const float lam = a.normq ? 1.0f / (qpi_abs / (float)B) : 1.0f;
     const float gpi = -lam * invEB;
-    for (int b = threadIdx.x; b < B; b += 256)
-        for (int e = 0; e < E; ++e) dq[e * a.dq.sy + B + b] = gpi;
+    if (!a.dq_fused)
+        for (int b = threadIdx.x; b < B; b += 256)
+            for (int e = 0; e < E; ++e) dq[e * a.dq.sy + B + b] = gpi;
     if (threadIdx.x == 0) {
         float* info = at(a.info, slot);
         info[0] = sq * invEB;

@@ -79,6 +79,7 @@ struct EngineOptions {
     int dw_tile_critic = 10, dw_tile_actor = 10;  // grouped dW tile ids (launch_gemm_group_dw)
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
     int dw_stagger = 0;    // fused dW + optimiser: first-wave start offsets (AdamEpi::stagger)
+    int fuse_dq = 0;       // critic-loss gradient seeds in the critic forward's head; loss_critic off the chain (measured -1.1 %)
     int bc_late = 0;       // BC loss / backward / optimiser after the critic forward (1) or backward (2)
     int xstep = 0;         // 1: each step's critic dW / optimiser + finalize at the head of the next
                            // step's graph (inside one fqlpop_step call; fqlpop::xstep)
@@ -101,6 +102,7 @@ const EngineOptionRef kEngineOptions[] = {
     {"dw_stagger", &EngineOptions::dw_stagger, 0, 256},
     {"xstep", &EngineOptions::xstep, 0, 1},
     {"bc_late", &EngineOptions::bc_late, 0, 2},
+    {"fuse_dq", &EngineOptions::fuse_dq, 0, 1},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -1280,11 +1282,23 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         launch_head_fwd(HEAD_STORE, ht, sX);
     }
     // ---- sM: critic on [s,a ; s,clip(a_pi)] -------------------------------
+    // fuse_dq: the head writes the critic-loss gradient seeds dq (elementwise given Q_target,
+    // which precedes it on sM), so the critic backward follows the forward directly and
+    // loss_critic (info, head-bias grad sums) runs off the chain on sF
+    const bool fdq = train && h->opt.fuse_dq && h->stream_fwd && h->stream_bwd && !h->cfg.normalize_q_loss &&
+                     sX == sM && NC.out_dim == 1;
     if (xin && sX != sM) HIPCHK(hipStreamWaitEvent(sM, h->ev_cdone, 0));
     {
         const NetLayout& N = NC;
         HeadArgs hc = head_args(c, N, h->cr_h[L - 1], B2, B2, sy2);
         hc.o0 = tref(h->q, (long long)E * B2, B2); hc.ld0 = B2;
+        if (fdq) {
+            hc.dq = la.dq; hc.qt = la.qt; hc.rew = la.rew; hc.mask = la.mask;
+            hc.discount = h->cfg.discount;
+            hc.inv_eb = 1.0f / (float)(E * B);
+            hc.gpi = -1.0f * hc.inv_eb;  // (normalize_q_loss off: lam = 1)
+            hc.q_min = h->cfg.q_agg_min; hc.E = E;
+        }
         if (h->stream_fwd) {
             // the a_pi columns [B, 2B) are back-propagated for dQ/da only: their layer outputs
             // (the dW GEMMs' operand) are not needed by the streamed backward
@@ -1302,7 +1316,14 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         dep(sM, sB);
         bc_chain();
     }
-    launch_loss_critic(la, sM);
+    if (fdq) {
+        la.dq_fused = 1;
+        dep(sM, sF);  // after the critic forward (sF is idle after the flow)
+        launch_loss_critic(la, sF);
+        HIPCHK(hipEventRecord(h->ev_flow, sF));  // the actor loss reads its info[7]; the critic optimiser its head-bias grads
+    } else {
+        launch_loss_critic(la, sM);
+    }
     // fused optimiser: the critic's dW + Adam is captured after the actor's dX
     // chain (it runs beside it instead of ahead of it on a shared queue)
     std::function<void()> critic_dw;
@@ -1352,8 +1373,12 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3,
                            B, B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, B, h->part_os, sM, nullptr,
                            &os_dw);
-            if (xout) h->xs_tail[h->cur] = critic_dw;  // (the next step's graph runs it)
-            else critic_dw();  // the fused launches include each net's small-leaf Adam
+            if (xout) {
+                h->xs_tail[h->cur] = critic_dw;  // (the next step's graph runs it)
+            } else {
+                if (fdq) HIPCHK(hipStreamWaitEvent(h->cdw_sb ? sB : sX, h->ev_flow, 0));  // g_cb4 (loss_critic)
+                critic_dw();  // the fused launches include each net's small-leaf Adam
+            }
             os_dw();
             if (xout) {
                 // this step's finalize runs in the next step's graph too: join the streams
