@@ -79,6 +79,8 @@ struct EngineOptions {
     int dw_tile_critic = 10, dw_tile_actor = 10;  // grouped dW tile ids (launch_gemm_group_dw)
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
     int dw_stagger = 0;    // fused dW + optimiser: first-wave start offsets (AdamEpi::stagger)
+    int early_join = 0;    // 1: the main chain waits for the flow and the BC loss before the critic loss /
+                           // backward (2: before the critic backward) instead of before the actor loss
     int fuse_dq = 0;       // critic-loss gradient seeds in the critic forward's head; loss_critic off the chain (measured -1.1 %)
     int bc_late = 0;       // BC loss / backward / optimiser after the critic forward (1) or backward (2)
     int xstep = 0;         // 1: each step's critic dW / optimiser + finalize at the head of the next
@@ -103,6 +105,7 @@ const EngineOptionRef kEngineOptions[] = {
     {"xstep", &EngineOptions::xstep, 0, 1},
     {"bc_late", &EngineOptions::bc_late, 0, 2},
     {"fuse_dq", &EngineOptions::fuse_dq, 0, 1},
+    {"early_join", &EngineOptions::early_join, 0, 2},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -1322,7 +1325,18 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         launch_loss_critic(la, sF);
         HIPCHK(hipEventRecord(h->ev_flow, sF));  // the actor loss reads its info[7]; the critic optimiser its head-bias grads
     } else {
+        if (h->opt.early_join == 1) {
+            HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
+            HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
+        }
         launch_loss_critic(la, sM);
+    }
+    if (h->opt.early_join == 2 && !fdq) {
+        // (the waits of the actor loss, moved ahead of the critic backward: a wait on a launch
+        // that finished long before resolves at once, while a wait on one that just finished
+        // on another queue costs that queue's signal latency, ~13 us in the step timeline)
+        HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
+        HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
     }
     // fused optimiser: the critic's dW + Adam is captured after the actor's dX
     // chain (it runs beside it instead of ahead of it on a shared queue)

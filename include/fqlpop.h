@@ -83,7 +83,8 @@ const char* fqlpop_last_error(void);
  *   xstep (0/1: inside one fqlpop_step call, each step's critic dW / optimiser runs at the
  *   head of the next step's graph, beside its sampling and actor forwards),
  *   bc_late (0..2: the BC update after the critic forward / backward of the main chain),
- *   fuse_dq (0/1: the critic-loss gradient seeds written by the critic forward's head).
+ *   fuse_dq (0/1: the critic-loss gradient seeds written by the critic forward's head),
+ *   early_join (0..2: the main chain's waits for the flow / BC loss moved ahead).
  * The defaults are the measured-fastest configuration.  Unknown names or values
  * out of range: FQLPOP_E_ARG.  The production library reads no environment
  * variable; result-changing timing switches exist only in diagnostic builds. */

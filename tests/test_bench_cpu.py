@@ -62,6 +62,7 @@ def test_schedule_experiment_options_default_off():
     assert fqlpop.get_engine_option("xstep") == 0
     assert fqlpop.get_engine_option("bc_late") == 0
     assert fqlpop.get_engine_option("fuse_dq") == 0
+    assert fqlpop.get_engine_option("early_join") == 0
     for name, hi in (("xstep", 1), ("bc_late", 2)):
         fqlpop.set_engine_option(name, hi)
         assert fqlpop.get_engine_option(name) == hi
