@@ -452,12 +452,13 @@ def test_cross_step_tail_bit_identical(calls):
     assert got[2][1] == ref[2][1] == steps, (got[2], ref[2])
 
 
-@pytest.mark.parametrize("mode", [1, 2])
-def test_bc_late_schedule_bit_identical(mode):
-    """Engine option bc_late (the BC update captured after the critic forward / backward) only
-    moves launches in the step's DAG: the same parameters, Adam state, target and info."""
+@pytest.mark.parametrize("opt", [{"bc_late": 1}, {"bc_late": 2}, {"early_join": 1}, {"early_join": 2}])
+def test_schedule_options_bit_identical(opt):
+    """Engine options bc_late (the BC update captured after the critic forward / backward) and
+    early_join (the main chain's waits for the flow / BC loss moved ahead) only move launches
+    or edges in the step's DAG: the same parameters, Adam state, target and info."""
     ref = _sampled_run(512, 256, 3, {})
-    got = _sampled_run(512, 256, 3, {"bc_late": mode})
+    got = _sampled_run(512, 256, 3, opt)
     assert np.array_equal(got[0], ref[0])
     for a, b in zip(got[1], ref[1]):
         assert np.array_equal(a, b)
