@@ -14,6 +14,7 @@ import pickle
 from copy import deepcopy
 from dataclasses import asdict
 from datetime import datetime
+import random
 from pathlib import Path
 
 import numpy as np
@@ -116,8 +117,19 @@ class Experiment:
                 seed = int(np.random.randint(0, 2**31 - 1)) if seed is None else int(seed)
                 eval_info = self.task.evaluate_members(self.agent.population, [self.agent.member], seed)[
                     self.agent.member]
+            elif seed is None:
+                eval_info, _ = evaluate_agent(agent=self.agent, env=self.task)
             else:
-                eval_info, _ = evaluate_agent(agent=self.agent, env=self.task, seed=seed)
+                # evaluate_actor_fn re-seeds random / np.random when given a seed (reference
+                # evaluator/evaluation.py:41-43); the reference's own evaluate() passes none
+                # (trainer/experiment.py:121), so its global streams (task.sample's batches, the
+                # checkpointed np_rng_state) never depend on the evaluations: keep them so here
+                py_state, np_state = random.getstate(), np.random.get_state()
+                try:
+                    eval_info, _ = evaluate_agent(agent=self.agent, env=self.task, seed=seed)
+                finally:
+                    random.setstate(py_state)
+                    np.random.set_state(np_state)
         self.logger.log(eval_info, step=self.current_step, group="eval")
         return eval_info.get("success", 0.0)
 
