@@ -5,9 +5,14 @@ One "step" = one population update: every member samples its own minibatch on
 device from the HBM-resident offline buffer and runs a full FQL ``update()``
 (critic TD loss, BC flow-matching loss, 10-step Euler flow, one-step
 distillation + Q loss, backward, Adam, target EMA).  ``value`` = member
-grad-steps per second over all ranks (weak scaling: 16 members per GPU).
+grad-steps per second over all ranks.
 
-  python bench.py [--gpus N --steps K --warmup W]
+Scaling (BASELINE north_star: "16-member alpha population at 1 GPU with >= 7x scaling at
+8 GPUs"): by default the 16-member population is sharded over the N ranks (strong scaling,
+16 / N members per GPU, ``--population``); ``--members M`` instead puts M members on every
+GPU (weak scaling, M * N members in all).
+
+  python bench.py [--gpus N --steps K --warmup W] [--population P | --members M]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py is its own
@@ -293,7 +298,11 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--members", type=int, default=16, help="population members per GPU")
+    ap.add_argument("--population", type=int, default=None,
+                    help="members of the whole population, sharded round-robin over the ranks (strong "
+                         "scaling; default 16, the north-star population)")
+    ap.add_argument("--members", type=int, default=None,
+                    help="members per GPU instead (weak scaling: members x N in all)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cube")
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--no-graph", action="store_true")
@@ -325,6 +334,8 @@ def main(argv=None):
     ap.add_argument("--diagnostic", action="store_true",
                     help="allow FQLPOP_* environment variables (developer A/B runs); they are recorded")
     args = ap.parse_args(argv)
+    if args.population is not None and args.members is not None:
+        ap.error("--population and --members are exclusive")
 
     fq_env = {k: v for k, v in os.environ.items() if k.startswith("FQLPOP_")}
     if fq_env and not args.diagnostic:
@@ -385,7 +396,12 @@ def main(argv=None):
     dev_data = D.broadcast_dataset(data, shapes, dev)
     torch.cuda.synchronize()
 
-    alphas_all, seeds_all = population_values(args.members * world)
+    weak = args.members is not None
+    n_total = args.members * world if weak else (args.population or 16)
+    if n_total < world:
+        log(f"bench.py: a {n_total}-member population cannot give every one of {world} ranks a member")
+        return 2
+    alphas_all, seeds_all = population_values(n_total)
     alphas, seeds = D.shard(alphas_all, rank, world), D.shard(seeds_all, rank, world)
     pcfg = PopulationConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"], batch_size=wl["batch_size"],
                             use_graph=not args.no_graph)
@@ -455,7 +471,7 @@ def main(argv=None):
     info = pop.read_info_array()
     finite = bool(np.all(np.isfinite(info[:, :13])))
 
-    member_steps = args.members * world * args.steps
+    member_steps = n_total * args.steps
     value = member_steps / el
     flops_ms = pop.flops_per_member_step
 
@@ -476,8 +492,8 @@ def main(argv=None):
             traffic = pmc["traffic_bytes_per_launch"]
 
     result = {
-        # BASELINE.json's metric at the default 16 members per GPU
-        "metric": f"FQL grad-steps/sec (whole node) over {args.members}-α population, "
+        # BASELINE.json's metric: the whole population (16 members by default) over all ranks
+        "metric": f"FQL grad-steps/sec (whole node) over {n_total}-α population, "
                   + ("cube-single-v0" if args.workload == "cube" else "antsoccer"),
         "value": round(value, 2),
         "unit": "member-grad-steps/s",
@@ -486,21 +502,26 @@ def main(argv=None):
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * el / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic ({args.rows / 1e6:g}M transitions of {args.workload} shape (obs {wl['obs_dim']}, act "
                 f"{wl['action_dim']}), seeded numpy; random-init weights)",
         "config": {
-            "workload": f"{wl['env']} {args.members}-alpha population update(), B={wl['batch_size']}, H=512x4, "
+            "workload": f"{wl['env']} {n_total}-alpha population update(), B={wl['batch_size']}, H=512x4, "
                         f"obs {wl['obs_dim']}, act {wl['action_dim']}, flow_steps 10",
-            "members_per_gpu": args.members,
-            "global_batch": wl["batch_size"] * args.members * world,
+            "population": n_total,
+            "members_per_gpu": (args.members if weak else
+                                (n_total // world if n_total % world == 0 else f"{n_total // world}-{-(-n_total // world)}")),
+            "members_this_rank": pop.n,
+            "global_batch": wl["batch_size"] * n_total,
             "population_steps_per_s": round(args.steps / el, 3),
             "gflop_per_member_step": round(flops_ms / 1e9, 4),
             "step_tflops": round(flops_ms * value / 1e12, 3),
             "step_mfma_frac": round(flops_ms * value / 1e12 / (MI355X_FP32_MFMA_PEAK_TFLOPS * world), 4),
-            "parallelism": f"weak: {args.members} members per GPU x {world} GPU(s), no data-path collective",
+            "parallelism": (f"weak: {args.members} members per GPU x {world} GPU(s)" if weak else
+                            f"strong: a {n_total}-member population sharded round-robin over {world} GPU(s)")
+                           + ", no data-path collective",
             "graph": not args.no_graph,
             "info_finite": finite,
             "share_device": bool(args.share_device),

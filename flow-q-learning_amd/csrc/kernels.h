@@ -90,7 +90,6 @@ struct AdamEpi {
     int mode;                         // 0; timing probes (FQLPOP_DW_MODE): 1 = no optimiser pass, 2 = one k-slice,
                                       // 3 = no W^T pass
     int nt;                           // non-temporal optimiser streams: 1 m/v, 2 target, 4 p_in, 8 p_out/W^T
-    int stagger;                      // first-wave start offsets (s_sleep 32 units per co-resident rank), 0 = off
     // the net's small leaves (biases, LN, head) ride in the same launch: blocks past the
     // GEMM tiles run the adam_kernel body on small.ids chunks (small_blocks = chunks x nz)
     AdamArgs small;
@@ -156,12 +155,6 @@ struct HeadArgs {         // out'[j][m] = sum_k W[k][j] h'[k][m] + b[j]
     float t_next;         // HEAD_EULER/BC_FUSED: time row value of the next step
     int ny, nz;
     const int* slots;
-    // HEAD_STORE of the critic forward with the critic-loss gradient seeds fused (dq.p set;
-    // nout 1, M = 2B, y = ensemble member): dq[y][m] = 2 (Q - target) / (E B) for the
-    // (s, a) columns m < B, gpi for the (s, a_pi) columns (loss_critic_kernel's values)
-    TRef dq, qt, rew, mask;
-    float discount, inv_eb, gpi;
-    int q_min, E;
 };
 void launch_head_fwd(int mode, const HeadArgs& a, hipStream_t s);
 
@@ -193,6 +186,31 @@ struct StreamArgs {
 };
 bool stream_fwd_supported(int H, int L, int K0, int nout, int M);
 void launch_stream_fwd(int head_mode, bool ln, const StreamArgs& a, hipStream_t s);
+
+// --------------------------------- split streamed forward (small populations) --
+// The streamed forward / persistent Euler flow with each 16-column tile computed by a
+// cluster of F = 2, 4 or 8 blocks that exchange every hidden layer's output through
+// L2 / MALL (kernels.hip, "split streamed forward"): bit-identical to the unsplit
+// kernels, and F times as many blocks, so that 1-4 members fill the chip.
+struct SplitSync {
+    float* xch;             // exchange, split_cluster_floats() per cluster
+    unsigned* cnt;          // arrival counters, split_counter_stride() apart, zeroed before every launch
+    unsigned* err;          // set to nonzero when a hand-off wait gives up (results then invalid)
+};
+struct SplitFwdArgs {
+    StreamArgs s;           // as launch_stream_fwd (Euler: params, w_off, b_off, x0 = state after step
+                            // first - 1 [D+A+1][B], K0 = D+A+1, L, M = B, ny = 1, head.nout = A)
+    TRef aflow;             // Euler: out [A][B]
+    int D, A, S, first;     // Euler: obs / action dims, flow steps, first step
+    float steps_f;
+    unsigned long long* probe;   // optional per-block {start, end} stamps
+    SplitSync sync;
+};
+long long split_cluster_floats();
+int split_counter_stride();
+bool split_fwd_supported(int H, int L, int K0, int nout, int M);
+// F = 8, 4 or 2 blocks per 16-column tile; grid = tiles x ny x nz x F blocks of 256 threads
+void launch_split_fwd(int head_mode, bool ln, bool euler, int F, const SplitFwdArgs& a, hipStream_t s);
 
 // ----------------------------------------------- streamed MLP backward ----
 // One launch = the whole dX chain of one network for all active members and
@@ -336,7 +354,6 @@ struct LossArgs {
     int B, A, E, da_n;
     int q_min, normq;
     float discount;
-    int dq_fused;                 // loss_critic: dq already written by the critic forward's head
     int nz;
     const int* slots;
 };

@@ -698,16 +698,6 @@ DEV void gemm_group_body(const GemmGroupArgs& ga, float* smem) {
         adam_chunk(ga.adam.small, sb % nch, sb / nch);
         return;
     }
-    if constexpr (EPI == EPI_ADAM) {
-        // staggered start of the first dispatch wave (blocks b, b + 256, b + 512, b + 768 share
-        // a CU): co-resident blocks then reach their HBM-bound optimiser pass at different
-        // times instead of all running the k-loop, then all streaming, in lock step
-        const int st = ga.adam.stagger;
-        if (st > 0 && (int)blockIdx.x < 1024) {
-            const int n = (((int)blockIdx.x >> 8) & 3) * st;
-            for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(32);
-        }
-    }
     const int bid = xcd_remap(blockIdx.x, ga.first[ga.ng]);
     int gi = 0;
 #pragma unroll
@@ -1320,23 +1310,6 @@ DEV void head_write(const HeadArgs& a, int slot, int y, int j, int m, float v) {
     const int B = a.B, D = a.D;
     if constexpr (MODE == HEAD_STORE) {
         at(a.o0, slot, y)[(long long)j * a.ld0 + m] = v;
-        if (a.dq.p != nullptr) {
-            // the critic-loss gradient seed of this Q, as loss_critic_kernel computes it
-            float g = a.gpi;
-            if (m < B) {
-                const float* qt = at(a.qt, slot);
-                float agg = a.q_min ? INFINITY : 0.f;
-                for (int e = 0; e < a.E; ++e) {
-                    const float u = qt[e * a.qt.sy + m];
-                    agg = a.q_min ? fminf(agg, u) : agg + u;
-                }
-                if (!a.q_min) agg /= (float)a.E;
-                const float yv = at(a.rew, slot)[m] + a.discount * at(a.mask, slot)[m] * agg;
-                const float d = v - yv;
-                g = 2.0f * d * a.inv_eb;
-            }
-            at(a.dq, slot, y)[m] = g;
-        }
     } else if constexpr (MODE == HEAD_ACT) {
         at(a.o0, slot, y)[(long long)j * a.ld0 + m] = clip1(v);
     } else if constexpr (MODE == HEAD_BC_FUSED) {
@@ -1616,6 +1589,503 @@ void launch_stream_fwd(int head_mode, bool ln, const StreamArgs& a, hipStream_t 
         default: if (ln) FQ_SF(HEAD_STORE, true); else FQ_SF(HEAD_STORE, false); break;
     }
 #undef FQ_SF
+}
+
+// ============================================ split streamed forward (small populations) ==
+// The streamed forward and the Euler flow with every 16-column tile computed by a CLUSTER of
+// F blocks (F = 2, 4 or 8), so that a population of one to four members still fills the chip
+// (the unsplit kernels give a 2-member population 32 to 128 blocks).  Block f of a cluster
+// owns the 512/F features [fb, fb + 512/F) of every hidden layer after the first; each of its
+// 4 waves runs TPW = 8/F 16x16 output tiles over the FULL K in the unsplit k order, so every
+// output element is the same fp32 chain as in stream_fwd_kernel / euler_flow_kernel: the
+// split results are bit-identical to the unsplit ones (and so independent of the split
+// chosen, the members per GPU and the world size).
+//   * layer 0 (K0 <= 64 inputs) is computed redundantly by every block of the cluster, with
+//     the unsplit lane layout (two "unsplit waves" per wave), into the LDS slab: no hand-off;
+//   * hidden layer l >= 1: A fragments W_l[4s + lk][feature] (TPW consecutive features per
+//     lane: dword / dwordx2 / dwordx4 loads, an 8-deep ring that runs across layers), B from
+//     the LDS slab; the epilogue publishes GELU(u) of the block's features to the cluster's
+//     exchange (write-through sc1 stores), and LayerNorm's column partials of the block's
+//     "unsplit waves", summed in the unsplit order from an LDS image of the block's tile;
+//   * hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, valid form 1): every storing
+//     wave drains (s_waitcnt vmcnt(0)), a barrier, ONE lane adds to the cluster's counter
+//     (agent-scope atomic); a consumer polls it (relaxed sc1 load + s_sleep, bounded), then
+//     stages the exchange into its LDS slab with sc1 loads (no plain load of handed-off bytes)
+//     and normalises it (LN: the 8 unsplit-wave partials summed in the unsplit order);
+//   * head: the Euler flow publishes every block's unsplit-wave head partials and every block
+//     sums the 8 in the unsplit order (x += v / S for the next step); the forward's head is
+//     computed by the cluster's LAST arriver (told by its counter add), which stages the last
+//     hidden layer, stores its G (and LN statistics) and calls head_write.
+// Counters are zeroed by a memset node before every launch; spins give up after ~2 s and
+// set sync.err (the runtime then reports an error instead of hanging).
+constexpr int SP_NW = 4, SP_NT = SP_NW * 64;
+constexpr long long SP_XB = (long long)EF_H * EF_NC;            // one hidden layer of a tile
+constexpr long long SP_HP = 2 * SP_XB;                          // head partials [8 waves][8 outputs][16]
+constexpr long long SP_LP = SP_HP + 8 * 8 * EF_NC;              // LN partials [2 parities][8 waves][2][16]
+constexpr long long SP_CLUSTER_FLOATS = SP_LP + 2 * 8 * 2 * EF_NC;
+constexpr int SP_CNT_STRIDE = 16;                               // counters 64 B apart
+constexpr unsigned SP_SPIN_LIMIT = 1u << 21;
+
+constexpr long long SP_CLUSTER_STRIDE = (SP_CLUSTER_FLOATS + 63) / 64 * 64;
+long long split_cluster_floats() { return SP_CLUSTER_STRIDE; }
+int split_counter_stride() { return SP_CNT_STRIDE; }
+
+typedef __attribute__((address_space(1))) unsigned int gu32_t;
+
+DEV unsigned sp_poll(const unsigned* cnt) {
+    return __hip_atomic_load((const gu32_t*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane 0 of the block waits until the cluster's counter reaches `target`; the barrier after it
+// releases the other waves (their loads of the exchange are all sc1)
+DEV void sp_wait(const SplitSync& sy, const unsigned* cnt, unsigned target) {
+    if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while (sp_poll(cnt) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > SP_SPIN_LIMIT) {
+                __hip_atomic_store((gu32_t*)sy.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
+}
+// every wave drains its sc1 stores, then one lane signals; returns the counter value before
+// this block's add (block-uniform via LDS)
+DEV unsigned sp_publish(unsigned* cnt, unsigned* bcast) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *bcast = __hip_atomic_fetch_add((gu32_t*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return *bcast;
+}
+DEV void sp_store1(rsrc_t r, float v, int off_b) {  // write-through (sc1) dword store
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, off_b, 0, 16);
+}
+DEV float4 sp_load4(rsrc_t r, int off_b) {  // sc1 (L1-bypassing) dwordx4 load
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off_b, 0, 16));
+}
+DEV float sp_load1(rsrc_t r, int off_b) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off_b, 0, 16));
+}
+
+// A fragments of TPW consecutive features: W[k][col .. col + TPW - 1] (components 0..TPW-1)
+template <int TPW>
+DEV float4 sp_aload(rsrc_t r, int elem_off) {
+    if constexpr (TPW == 4) {
+        return bload4(r, elem_off);
+    } else if constexpr (TPW == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, elem_off * 4, 0, 0);
+        const float2 f = __builtin_bit_cast(float2, v);
+        return float4{f.x, f.y, 0.f, 0.f};
+    } else {
+        return float4{bload1(r, elem_off * 4, 0), 0.f, 0.f, 0.f};
+    }
+}
+
+// One split hidden layer's k-loop (see ef_kloop): acc[t] += W[k][col + t] xs[k][li] over the
+// NS k-steps; ring[] holds this layer's first SP_PF k-steps on entry and the next layer's
+// (w_next) on exit.  lo = lk * H + col.
+constexpr int SP_PF = 8;
+template <int TPW>
+DEV void sp_kloop(f32x4 (&acc)[TPW], float4 (&ring)[SP_PF], rsrc_t rW, const float* xs, int NS, int w_cur,
+                  int w_next, int lo, int lk, int li) {
+    constexpr int H = EF_H, NC = EF_NC, PF = SP_PF;
+    float bnext = xs[lk * NC + li];
+    int s0 = 0;
+    do {
+        const int rbase = (s0 + PF < NS ? w_cur + 4 * (s0 + PF) * H : w_next) + lo;
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            const int s = s0 + p;
+            const float b = bnext;
+            bnext = xs[(4 * (s + 1) + lk) * NC + li];
+            __builtin_amdgcn_sched_barrier(0);
+            const float4 a = ring[p];
+            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b, acc[0], 0, 0, 0);
+            if constexpr (TPW > 1) acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b, acc[1], 0, 0, 0);
+            if constexpr (TPW > 2) {
+                acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b, acc[2], 0, 0, 0);
+                acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b, acc[3], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            ring[p] = sp_aload<TPW>(rW, rbase + 4 * p * H);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        s0 += PF;
+    } while (s0 < NS);
+}
+
+bool split_fwd_supported(int H, int L, int K0, int nout, int M) {
+    // L >= 3: a hand-off wait lies between two steps' head-partial writes (Euler)
+    return H == EF_H && L >= 3 && L <= EF_MAX_LAYERS && K0 <= EF_K0MAX && nout <= 8 && M % EF_NC == 0;
+}
+
+template <int MODE, bool LN, bool EULER, int TPW>
+__global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs a) {
+    constexpr int H = EF_H, NC = EF_NC, NT = SP_NT, PF = EF_PF, F = 8 / TPW, FB = H / F;
+    const StreamArgs& g = a.s;
+    __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];         // layer input [H][NC] (+ look-ahead slack)
+    __shared__ __attribute__((aligned(16))) float in0[EF_K0MAX * NC + 64];   // layer-0 input
+    __shared__ __attribute__((aligned(16))) float tile[FB * NC];             // the block's layer output (LN / head)
+    __shared__ float lnred[2][8][NC];                                        // unsplit-wave LN partials
+    __shared__ float stat[2][NC];                                            // column mean / rstd
+    __shared__ float hred[8][8][NC];                                         // unsplit-wave head partials
+    __shared__ unsigned bc;
+
+    const int tiles = g.M / NC;
+    const int cl = blockIdx.x / F, f = blockIdx.x % F, fb = f * FB;
+    const int tl = cl % tiles, yz = cl / tiles;
+    const int y = yz % g.ny, z = yz / g.ny;
+    const int slot = g.slots[z];
+    const int c0 = tl * NC;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    const int L = g.L, K0 = g.K0, nout = g.head.nout;
+    if (a.probe != nullptr && tid == 0) a.probe[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    const bool tail0 = K0 > 4 * PF && K0 <= 4 * (PF + 1);
+    const int NS0 = tail0 ? PF : (K0 + 4 * PF - 1) / (4 * PF) * PF;
+    const float* __restrict__ P = g.params + (long long)slot * g.P + (long long)y * g.ens;
+    const rsrc_t rW = make_rsrc(P, g.P);
+    float* const X = a.sync.xch + (long long)cl * SP_CLUSTER_STRIDE;
+    const rsrc_t rX = make_rsrc(X, SP_CLUSTER_FLOATS);
+    unsigned* const cnt = a.sync.cnt + (long long)cl * SP_CNT_STRIDE;
+    unsigned npub = 0;  // hand-offs published by every block of the cluster so far
+    const bool st = c0 >= g.st_lo && c0 + NC <= g.st_hi;
+    const long long sbase = (long long)slot * g.s_ss + (long long)y * g.s_sy + c0;
+    // head A fragments of the block's unsplit waves (Euler: used every step)
+    load_in0<NT>(in0, g.x0 + (long long)slot * g.x0_ss, K0, g.ld_x, c0);
+    __syncthreads();
+
+    // LayerNorm statistics of one column from the 8 unsplit-wave partials (stream_fwd_kernel's sums)
+    auto col_stats = [&](int col, float& mean, float& rs) {
+        float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+        for (int w8 = 0; w8 < EF_NW; ++w8) {
+            S1 += lnred[0][w8][col];
+            S2 += lnred[1][w8][col];
+        }
+        mean = S1 / (float)H;
+        const float var = fmaxf(S2 / (float)H - mean * mean, 0.f);
+        rs = 1.0f / sqrtf(var + 1e-6f);
+    };
+    // normalise the slab in place (thread: features 2 tid, 2 tid + 1) with the statistics in stat[]
+    auto ln_slab = [&](int l) {
+        const float2 ga = *reinterpret_cast<const float2*>(&P[g.g_off[l] + 2 * tid]);
+        const float2 be = *reinterpret_cast<const float2*>(&P[g.be_off[l] + 2 * tid]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float gv = h ? ga.y : ga.x, bv = h ? be.y : be.x;
+            float* row = &slab[(2 * tid + h) * NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) row[c] = (row[c] - stat[0][c]) * stat[1][c] * gv + bv;
+        }
+    };
+    // the block's feature slice of a layer output in the slab -> G (and the LN stats -> MU / RS)
+    auto store_slab_slice = [&](int l) {
+        if (!st || g.G[l] == nullptr || c0 + NC > g.g_hi) return;
+        float* Gp = g.G[l] + sbase;
+        for (int e = tid; e < FB * NC / 4; e += NT) {
+            const int fr = fb + e / (NC / 4), c4 = (e % (NC / 4)) * 4;
+            *reinterpret_cast<float4*>(&Gp[(long long)fr * g.ld_s + c4]) = *reinterpret_cast<const float4*>(&slab[fr * NC + c4]);
+        }
+    };
+    auto store_stats = [&](int l) {
+        if (LN && st && f == 0 && tid < NC && g.MU[l]) {
+            const long long so = (long long)slot * g.st_ss + (long long)y * g.st_sy + c0 + tid;
+            g.MU[l][so] = stat[0][tid];
+            g.RS[l][so] = stat[1][tid];
+        }
+    };
+    // stage a published layer output (+ LN partials) from the exchange into the slab
+    auto stage = [&](int par) {
+#pragma unroll
+        for (int i = 0; i < (int)(SP_XB / 4 / NT); ++i) {
+            const int e = tid + i * NT;
+            reinterpret_cast<float4*>(slab)[e] = sp_load4(rX, (int)((par * SP_XB) * 4) + e * 16);
+        }
+        if (LN) {  // the exchange holds [w][s][c] (tid < 256 = 8 x 2 x 16); lnred is [s][w][c]
+            const float v = sp_load1(rX, (int)((SP_LP + par * 8 * 2 * NC) * 4) + tid * 4);
+            lnred[(tid / NC) & 1][tid / (2 * NC)][tid % NC] = v;
+        }
+        __syncthreads();
+        if (LN) {
+            if (tid < NC) col_stats(tid, stat[0][tid], stat[1][tid]);
+            __syncthreads();
+        }
+    };
+
+    const int EUS = EULER ? a.S : 1;
+    for (int step = EULER ? a.first : 0; step < EUS; ++step) {
+        if (EULER && step == a.first) {
+            if (tid < NC) in0[(a.D + a.A) * NC + tid] = (float)((double)step / (double)a.S);
+            __syncthreads();
+        }
+        // ---- layer 0, redundantly in every block: unsplit waves 2q, 2q + 1 ----
+        {
+            float v[2][4][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int w = 2 * q + h;
+                const int lo = lk * H + 64 * w + 4 * li;
+                float4 ring[PF];
+#pragma unroll
+                for (int p = 0; p < PF; ++p) ring[p] = bload4(rW, (int)g.w_off[0] + 4 * p * H + lo);
+                const float4 at0 = bload4(rW, (int)g.w_off[0] + 4 * PF * H + lo);
+                float4 bias4[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) bias4[r] = bload4(rW, (int)g.b_off[0] + 64 * w + 16 * lk + 4 * r);
+                f32x4 acc[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+                ef_kloop(acc, ring, rW, in0, NS0, (int)g.w_off[0], (int)g.w_off[0], lo, lk, li);
+                if (tail0) ef_tail(acc, at0, in0, lk, li);
+                const bool stU = st && g.U[0] && 64 * w >= fb && 64 * w < fb + FB;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float bv[4] = {bias4[r].x, bias4[r].y, bias4[r].z, bias4[r].w};
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const float u = acc[c][r] + bv[c];
+                        if (stU) g.U[0][sbase + (long long)(64 * w + 16 * lk + 4 * r + c) * g.ld_s + li] = u;
+                        v[h][r][c] = gelu_fast(u);
+                    }
+                }
+                if constexpr (LN) {
+                    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            s1 += v[h][r][c];
+                            s2 += v[h][r][c] * v[h][r][c];
+                        }
+                    s1 = lk_sum(s1);
+                    s2 = lk_sum(s2);
+                    if (lk == 0) {
+                        lnred[0][w][li] = s1;
+                        lnred[1][w][li] = s2;
+                    }
+                }
+            }
+            __syncthreads();  // lnred visible; every wave is done reading the slab (previous layer)
+            float mean = 0.f, rs = 0.f;
+            if constexpr (LN) col_stats(li, mean, rs);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int w = 2 * q + h;
+                float ga[16], be[16];
+                if constexpr (LN) {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        ga[e] = P[g.g_off[0] + 64 * w + 16 * lk + e];
+                        be[e] = P[g.be_off[0] + 64 * w + 16 * lk + e];
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        float x = v[h][r][c];
+                        if constexpr (LN) x = (x - mean) * rs * ga[4 * r + c] + be[4 * r + c];
+                        slab[(64 * w + 16 * lk + 4 * r + c) * NC + li] = x;
+                    }
+            }
+            if constexpr (LN) {
+                if (tid < NC) {
+                    col_stats(tid, stat[0][tid], stat[1][tid]);
+                }
+            }
+            __syncthreads();
+            if (!EULER) {
+                store_slab_slice(0);
+                store_stats(0);
+            }
+        }
+        // ---- hidden layers 1 .. L-1, split ----
+        float4 ring[SP_PF];
+        const int col = fb + 16 * TPW * q + TPW * li;
+        const int lo = lk * H + col;
+#pragma unroll
+        for (int p = 0; p < SP_PF; ++p) ring[p] = sp_aload<TPW>(rW, (int)g.w_off[1] + 4 * p * H + lo);
+        for (int l = 1; l < L; ++l) {
+            if (l >= 2) {
+                sp_wait(a.sync, cnt, (unsigned)F * npub);
+                stage((l - 1) & 1);
+                if constexpr (LN) {
+                    ln_slab(l - 1);
+                    __syncthreads();
+                    // (without LN the producers stored G_{l-1} themselves)
+                    store_slab_slice(l - 1);
+                    store_stats(l - 1);
+                }
+            }
+            f32x4 acc[TPW];
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            // bias of the lane's 4 TPW features fb + 16 TPW q + 4 TPW lk + (TPW r + t)
+            float bias[4 * TPW];
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+                const float4 b4 = bload4(rW, (int)g.b_off[l] + fb + 16 * TPW * q + 4 * TPW * lk + 4 * i);
+                bias[4 * i] = b4.x; bias[4 * i + 1] = b4.y; bias[4 * i + 2] = b4.z; bias[4 * i + 3] = b4.w;
+            }
+            const int wcur = (int)g.w_off[l], wnext = (int)g.w_off[l + 1 < L ? l + 1 : 1];
+            asm volatile("" ::"s"(wcur), "s"(wnext));
+            sp_kloop<TPW>(acc, ring, rW, slab, H / 4, wcur, wnext, lo, lk, li);
+            // epilogue: tile t, reg r: feature fb + 16 TPW q + TPW (4 lk + r) + t, column li
+            const bool last = l == L - 1;
+            const bool stU = st && g.U[l];
+            const bool stG = !LN && st && g.G[l] && c0 + NC <= g.g_hi;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) {
+                    const int fl = 16 * TPW * q + TPW * (4 * lk + r) + t;  // feature - fb
+                    const float u = acc[t][r] + bias[TPW * r + t];
+                    if (stU) g.U[l][sbase + (long long)(fb + fl) * g.ld_s + li] = u;
+                    const float gv = gelu_fast(u);
+                    if (stG) g.G[l][sbase + (long long)(fb + fl) * g.ld_s + li] = gv;
+                    tile[fl * NC + li] = gv;
+                    if (!EULER || !last) sp_store1(rX, gv, (int)(((l & 1) * SP_XB + (long long)(fb + fl) * NC + li) * 4));
+                }
+            __syncthreads();  // tile complete
+            if (LN && q < TPW) {
+                // LN partials of unsplit wave f TPW + q, in its order (features 64 q + 16 lk + e)
+                float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const float x = tile[(64 * q + 16 * lk + e) * NC + li];
+                    s1 += x;
+                    s2 += x * x;
+                }
+                s1 = lk_sum(s1);
+                s2 = lk_sum(s2);
+                if (lk == 0) {
+                    const int w8 = f * TPW + q;
+                    sp_store1(rX, s1, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + li) * 4));
+                    sp_store1(rX, s2, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + NC + li) * 4));
+                }
+            }
+            if (EULER && last && q < TPW) {
+                // head partials of unsplit wave f TPW + q (euler_flow_kernel's head)
+                const int w8 = f * TPW + q;
+                float w5r[16];
+#pragma unroll
+                for (int s = 0; s < 16; ++s) w5r[s] = bload1(rW, ((int)g.w_off[L] + (64 * w8 + 4 * s + lk) * a.A + li) * 4, 0);
+#pragma unroll
+                for (int s = 0; s < 16; ++s) w5r[s] = li < a.A ? w5r[s] : 0.f;
+                f32x4 hacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < 16; ++s)
+                    hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(w5r[s], tile[(64 * q + 4 * s + lk) * NC + li], hacc, 0, 0, 0);
+                if (lk < 2) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        sp_store1(rX, hacc[r], (int)((SP_HP + (w8 * 8 + 4 * lk + r) * NC + li) * 4));
+                }
+            }
+            ++npub;
+            const unsigned before = sp_publish(cnt, &bc);
+            if (!EULER && last) {
+                // the cluster's last arriver: stage the last hidden layer, store it, run the head
+                if (before != (unsigned)F * npub - 1) break;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                stage(l & 1);
+                if constexpr (LN) ln_slab(l);
+                __syncthreads();
+                if (LN && st && g.G[l] && c0 + NC <= g.g_hi) {
+                    float* Gp = g.G[l] + sbase;
+                    for (int e = tid; e < H * NC / 4; e += NT) {
+                        const int fr = e / (NC / 4), c4 = (e % (NC / 4)) * 4;
+                        *reinterpret_cast<float4*>(&Gp[(long long)fr * g.ld_s + c4]) =
+                            *reinterpret_cast<const float4*>(&slab[fr * NC + c4]);
+                    }
+                }
+                if (LN && st && tid < NC && g.MU[l]) {
+                    const long long so = (long long)slot * g.st_ss + (long long)y * g.st_sy + c0 + tid;
+                    g.MU[l][so] = stat[0][tid];
+                    g.RS[l][so] = stat[1][tid];
+                }
+                // head partials of all 8 unsplit waves (wave q: 2q, 2q + 1), stream_fwd_kernel's order
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int w8 = 2 * q + h;
+                    float w5r[16];
+#pragma unroll
+                    for (int s = 0; s < 16; ++s) w5r[s] = bload1(rW, ((int)g.w_off[L] + (64 * w8 + 4 * s + lk) * nout + li) * 4, 0);
+#pragma unroll
+                    for (int s = 0; s < 16; ++s) w5r[s] = li < nout ? w5r[s] : 0.f;
+                    f32x4 hacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s = 0; s < 16; ++s)
+                        hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(w5r[s], slab[(64 * w8 + 4 * s + lk) * NC + li], hacc, 0, 0, 0);
+                    if (lk < 2) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) hred[w8][4 * lk + r][li] = hacc[r];
+                    }
+                }
+                __syncthreads();
+                if (tid < nout * NC) {
+                    const int j = tid / NC, cc = tid % NC;
+                    float v = hred[0][j][cc];
+#pragma unroll
+                    for (int w8 = 1; w8 < EF_NW; ++w8) v += hred[w8][j][cc];
+                    v += P[g.b_off[L] + j];
+                    head_write<MODE>(g.head, slot, y, j, c0 + cc, v);
+                }
+            }
+        }
+        if constexpr (EULER) {
+            // every block: the 8 unsplit-wave head partials, summed in euler_flow_kernel's order
+            sp_wait(a.sync, cnt, (unsigned)F * npub);
+            if (tid < a.A * NC) {
+                const int aa = tid / NC, j = tid % NC;
+                float v = sp_load1(rX, (int)((SP_HP + aa * NC + j) * 4));
+#pragma unroll
+                for (int w8 = 1; w8 < EF_NW; ++w8) v += sp_load1(rX, (int)((SP_HP + (w8 * 8 + aa) * NC + j) * 4));
+                v += P[g.b_off[L] + aa];
+                float* xp = &in0[(a.D + aa) * NC + j];
+                *xp = *xp + v / a.steps_f;
+            } else if (tid < (a.A + 1) * NC && step + 1 < a.S) {
+                in0[(a.D + a.A) * NC + tid - a.A * NC] = (float)((double)(step + 1) / (double)a.S);
+            }
+            __syncthreads();
+        }
+    }
+    if (EULER && f == 0 && tid < a.A * NC) {
+        const int aa = tid / NC, j = tid % NC;
+        at(a.aflow, slot)[(long long)aa * a.s.M + c0 + j] = clip1(in0[(a.D + aa) * NC + j]);
+    }
+    if (a.probe != nullptr) {
+        __syncthreads();
+        if (tid == 0) a.probe[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+void launch_split_fwd(int head_mode, bool ln, bool euler, int F, const SplitFwdArgs& a, hipStream_t s) {
+    const dim3 grid((a.s.M / EF_NC) * a.s.ny * a.s.nz * F), block(SP_NT);
+#define FQ_SPF(MODE, LNV, EU, T) hipLaunchKernelGGL((split_fwd_kernel<MODE, LNV, EU, T>), grid, block, 0, s, a)
+#define FQ_SPF_T(MODE, LNV, EU)                          \
+    switch (F) {                                         \
+        case 8: FQ_SPF(MODE, LNV, EU, 1); break;         \
+        case 4: FQ_SPF(MODE, LNV, EU, 2); break;         \
+        default: FQ_SPF(MODE, LNV, EU, 4); break;        \
+    }
+    if (euler) {
+        FQ_SPF_T(HEAD_EULER, false, true)
+    } else {
+        switch (head_mode) {
+            case HEAD_BC_FUSED: if (ln) { FQ_SPF_T(HEAD_BC_FUSED, true, false) } else { FQ_SPF_T(HEAD_BC_FUSED, false, false) } break;
+            case HEAD_OS: if (ln) { FQ_SPF_T(HEAD_OS, true, false) } else { FQ_SPF_T(HEAD_OS, false, false) } break;
+            default: if (ln) { FQ_SPF_T(HEAD_STORE, true, false) } else { FQ_SPF_T(HEAD_STORE, false, false) } break;
+        }
+    }
+#undef FQ_SPF_T
+#undef FQ_SPF
 }
 
 // ============================================================ backward =====
@@ -2513,7 +2983,7 @@ __global__ __launch_bounds__(256) void loss_critic_kernel(const LossArgs a) {
             qmx = fmaxf(qmx, qv);
             qmn = fminf(qmn, qv);
             const float g = 2.0f * d * invEB;
-            if (!a.dq_fused) dq[e * a.dq.sy + b] = g;
+            dq[e * a.dq.sy + b] = g;
             if (e < 4) sdq[e] += g;
             qp += q[e * a.q.sy + B + b];
         }
@@ -2543,9 +3013,8 @@ __global__ __launch_bounds__(256) void loss_critic_kernel(const LossArgs a) {
     const float qmean_pi = qpi_s / (float)B;
     const float lam = a.normq ? 1.0f / (qpi_abs / (float)B) : 1.0f;
     const float gpi = -lam * invEB;
-    if (!a.dq_fused)
-        for (int b = threadIdx.x; b < B; b += 256)
-            for (int e = 0; e < E; ++e) dq[e * a.dq.sy + B + b] = gpi;
+    for (int b = threadIdx.x; b < B; b += 256)
+        for (int e = 0; e < E; ++e) dq[e * a.dq.sy + B + b] = gpi;
     if (threadIdx.x == 0) {
         float* info = at(a.info, slot);
         info[0] = sq * invEB;

@@ -72,20 +72,17 @@ struct EngineOptions {
     int stream_fwd = 1;    // whole-network forward launches
     int stream_bwd = 1;    // whole-network dX chains
     int fused_adam = 1;    // optimiser in the grouped dW epilogue
-    int cdw_sb = 1;        // critic dW + optimiser on the BC stream, beside the actor chain
     int serial = 0;        // every launch on one stream (uncontended kernel traces)
-    int streams = 3;       // 4: target critic + dW/optimiser on a 4th stream
-    int prio = 0;          // stream priorities: 1 main chain high, 2 flow high
     int dw_tile_critic = 10, dw_tile_actor = 10;  // grouped dW tile ids (launch_gemm_group_dw)
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
-    int dw_stagger = 0;    // fused dW + optimiser: first-wave start offsets (AdamEpi::stagger)
-    int early_join = 0;    // 1: the main chain waits for the flow and the BC loss before the critic loss /
-                           // backward (2: before the critic backward) instead of before the actor loss
-    int fuse_dq = 0;       // critic-loss gradient seeds in the critic forward's head; loss_critic off the chain (measured -1.1 %)
-    int bc_late = 0;       // BC loss / backward / optimiser after the critic forward (1) or backward (2)
-    int xstep = 0;         // 1: each step's critic dW / optimiser + finalize at the head of the next
-                           // step's graph (inside one fqlpop_step call; fqlpop::xstep)
+    int split = 1;         // small populations: streamed forwards / Euler flow as clusters of 2-8 blocks per
+                           // 16-column tile (bit-identical); 0 off, 1 auto, 2 / 4 / 8 blocks where they fit
 };
+// (Schedule experiments that measured slower were removed in round 4 and stay in git history
+// and DESIGN.md section 5: a 4th stream, stream priorities, the critic optimiser on the main
+// chain's queue, first-wave staggering of the fused dW launch, the cross-step critic tail,
+// the BC update late in the step, the critic-loss seeds in the critic forward's head, and the
+// main chain's early joins.)
 EngineOptions g_engine_opts;
 
 struct EngineOptionRef {
@@ -96,16 +93,11 @@ struct EngineOptionRef {
 const EngineOptionRef kEngineOptions[] = {
     {"euler_fused", &EngineOptions::euler_fused, 0, 1}, {"stream_fwd", &EngineOptions::stream_fwd, 0, 1},
     {"stream_bwd", &EngineOptions::stream_bwd, 0, 1},   {"fused_adam", &EngineOptions::fused_adam, 0, 1},
-    {"cdw_sb", &EngineOptions::cdw_sb, 0, 1},           {"serial", &EngineOptions::serial, 0, 1},
-    {"streams", &EngineOptions::streams, 3, 4},         {"prio", &EngineOptions::prio, 0, 2},
+    {"serial", &EngineOptions::serial, 0, 1},
     {"dw_tile_critic", &EngineOptions::dw_tile_critic, 0, 10},
     {"dw_tile_actor", &EngineOptions::dw_tile_actor, 0, 10},
     {"adam_nt", &EngineOptions::adam_nt, 0, 3},
-    {"dw_stagger", &EngineOptions::dw_stagger, 0, 256},
-    {"xstep", &EngineOptions::xstep, 0, 1},
-    {"bc_late", &EngineOptions::bc_late, 0, 2},
-    {"fuse_dq", &EngineOptions::fuse_dq, 0, 1},
-    {"early_join", &EngineOptions::early_join, 0, 2},
+    {"split", &EngineOptions::split, 0, 8},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -219,7 +211,6 @@ struct fqlpop {
     // fused optimiser (Adam in the dW epilogue): stats chunk id of each net's
     // W_l tiles, and the remaining (small-leaf) chunks the adam kernel runs
     bool fused_adam = false;
-    bool cdw_sb = true;            // the critic's fused dW + optimiser on sB (beside the actor chain)
     int w_stat_base[3][EF_MAX_LAYERS] = {};
     int* res_ids = nullptr;
     int res_base[3] = {0, 0, 0}, res_n[3] = {0, 0, 0};
@@ -250,27 +241,24 @@ struct fqlpop {
     float *inj_batch = nullptr, *inj_noise = nullptr;
     long long inj_bs = 0, inj_ns = 0;
 
-    hipStream_t sM = nullptr, sF = nullptr, sB = nullptr, sX = nullptr;
-    hipEvent_t ev_sample, ev_bcfwd, ev_bcloss, ev_flow, ev_bdone, ev_t0, ev_t1;
-    // cross-step critic tail (engine option xstep): inside one fqlpop_step call, every step but
-    // the last leaves its critic partial fold + fused dW / optimiser and the grad-stat finalize
-    // out of its graph (xs_out); the next step's graph runs them on sB at its head (xs_in),
-    // beside its sampling, one-step and BC forwards and flow, and its target-critic and critic
-    // forwards wait for them (ev_cdone).  The sampler of an xs_in step reads count + 1 before
-    // that finalize increments count (finalize waits for the sampler).  cr_in alternates with
-    // the parameter buffer, so the next sampler never writes the dW's layer-0 operand.
-    bool xstep = false;
-    bool xs_in = false, xs_out = false;    // flags of the step being enqueued
-    bool skip_dw_wait = false;             // the deferred dW half runs in the next graph
-    std::function<void()> xs_tail[2];      // deferred critic dW half, per parameter buffer
-    std::set<long long> xs_built;          // (active count, probe set) with every variant captured
-    hipEvent_t ev_cdone = nullptr;
+    hipStream_t sM = nullptr, sF = nullptr, sB = nullptr;
+    hipEvent_t ev_sample, ev_bcfwd, ev_bcloss, ev_flow, ev_bdone;
+    hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;  // fqlpop_time_dominant_kernel
     std::vector<hipEvent_t> ev_pool;
     int ev_next = 0;
     // in-step timing probe of the dominant kernel (Euler hidden-layer GEMM):
     // its blocks stamp s_memrealtime into per-launch slots; two slot sets are
     // used by alternate steps so the host reads step i-2 while step i runs
     bool euler_fused = false;      // Euler steps 1..S-1 as one persistent launch (euler_flow_kernel)
+    // split launches (engine option split): per launch site an exchange area and a block of
+    // arrival counters (zeroed by a memset node before every launch), and one error word
+    struct SplitSite {
+        float* xch = nullptr;
+        unsigned* cnt = nullptr;
+        long long clusters = 0;    // capacity
+    } split_site[5];
+    unsigned* split_err = nullptr;
+    bool split_ok = false;
     bool stream_fwd = false;       // whole-network forward launches (stream_fwd_kernel)
     bool stream_bwd = false;       // whole-network dX chains (stream_bwd_kernel)
     float *part_cr = nullptr, *part_bc = nullptr, *part_os = nullptr;  // stream_bwd column-sum partials
@@ -285,8 +273,6 @@ struct fqlpop {
     RolloutArgs em_args{};
     bool em_set = false;
     bool probe = false;
-    int pipe_exp = 0;
-    bool pipe_started = false;  // FQLPOP_PIPE_EXP timing experiment (eager, racy)
     int probe_set = -1;            // set used by the step being enqueued (-1: none)
     int probe_idx = 0;             // next launch slot of that set
     long long probe_step = 0;
@@ -302,7 +288,7 @@ struct fqlpop {
     long long ephase_blocks = 0;
     int probe_pairs = 0;
     long long probe_blocks = 0;                  // max blocks of one dominant-kernel launch
-    int probe_nz[2] = {0, 0};                    // active members of the step that used each set
+    long long probe_nb[2] = {0, 0};              // blocks of the dominant launch of the step that used each set
     hipEvent_t probe_done[2] = {nullptr, nullptr};
     hipStream_t probe_stream = nullptr;
     bool probe_pending[2] = {false, false};
@@ -750,7 +736,7 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
     // captured ahead of it
     const int NP = a.NP;
     auto dw_half = [=, &N]() {
-    if (ev && !h->skip_dw_wait) HIPCHK(hipStreamWaitEvent(sw, ev, 0));
+    if (ev) HIPCHK(hipStreamWaitEvent(sw, ev, 0));
     ColsumArgs r{};
     r.part = part; r.NP = NP; r.tiles = Mg / 16;
     r.grads = h->grads + N.off; r.P = h->P; r.ens = N.ens_size;
@@ -803,7 +789,6 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
             // need not displace the weights the streamed kernels re-read from L2 / MALL
             // (+1.0 % same-box; engine option adam_nt: bit mask, see AdamEpi::nt)
             ae.nt = h->opt.adam_nt;
-            ae.stagger = h->opt.dw_stagger;
         }
         ae.small = adam_args(c, ni);
         ae.small_blocks = ae.small.n_chunks * c.nz;
@@ -879,6 +864,38 @@ void adam_net(const Ctx& c, hipStream_t s, int ni) {
     if (a.n_chunks > 0) launch_adam(a, s);
 }
 
+// Split launch sites (fqlpop::split_site): BC forward, Euler flow (sF); one-step, target
+// critic, critic forwards (sM).
+enum { SITE_BCF = 0, SITE_EULER = 1, SITE_OSF = 2, SITE_TGT = 3, SITE_CRF = 4, SITE_N = 5 };
+constexpr long long kSplitMaxClusters = 128;  // a site with more 16-column tiles runs unsplit
+constexpr long long kSplitMaxBlocks = 256;    // one block per CU (see split_factor)
+
+// Blocks per 16-column tile of a split launch (1 = the unsplit kernel).  Only where the
+// unsplit kernel leaves CUs idle (<= 128 tiles); the most of 8, 4, 2 blocks that keeps the
+// launch within 256 blocks (forced values shrink to fit).  The split kernel runs 2 waves per
+// SIMD and <= 59 KB of LDS per block, so the split launches of the two streams that can run
+// at once (sF, sM) fit the chip together and every cluster's blocks are resident at the same
+// time (their hand-off waits need that).  The Euler flow uses 4 or 8 (its 2-block form
+// would spill).
+int split_factor(const fqlpop* h, long long clusters, bool euler) {
+    const int opt = h->opt.split;
+    if (!h->split_ok || opt == 0 || clusters > kSplitMaxClusters) return 1;
+    for (int F = opt >= 2 ? opt : 8; F >= 2; F /= 2) {
+        if (euler && F < 4) break;
+        if (clusters * F <= kSplitMaxBlocks) return F;
+    }
+    return 1;
+}
+
+// The site's synchronisation state for one launch over `clusters` tiles: its counters are
+// zeroed on `s` first (a memset node in the step's graph).
+SplitSync split_prep(fqlpop* h, int site, long long clusters, hipStream_t s) {
+    fqlpop::SplitSite& st = h->split_site[site];
+    ARGCHK(clusters <= st.clusters, "split launch larger than its site");
+    HIPCHK(hipMemsetAsync(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * clusters, s));
+    return SplitSync{st.xch, st.cnt, h->split_err};
+}
+
 // One whole-network forward launch (stream_fwd_kernel).  `arena` + N.off is the
 // net's parameter block (slot stride P); activations for the backward pass are
 // stored for columns [st_lo, st_hi) into U/G (slot stride s_ss, ensemble
@@ -917,8 +934,47 @@ void stream_fwd(const Ctx& c, hipStream_t s, const NetLayout& N, const float* ar
     a.ny = N.E; a.nz = c.nz; a.slots = h->slots;
     const int sk = skip_mask();
     const int bit = &N == &h->bc ? 16 : &N == &h->os ? 8 : arena == h->target ? 2 : 4;
-    if (!(sk & bit)) launch_stream_fwd(mode, N.ln, a, s);
+    if (sk & bit) return;
+    const int site = &N == &h->bc ? SITE_BCF : &N == &h->os ? SITE_OSF : arena == h->target ? SITE_TGT : SITE_CRF;
+    const long long clusters = (long long)(M / 16) * N.E * c.nz;
+    const int F = split_fwd_supported(N.H, N.L, N.in_dim, N.out_dim, M) ? split_factor(h, clusters, false) : 1;
+    if (F > 1) {
+        SplitFwdArgs sa{};
+        sa.s = a;
+        sa.sync = split_prep(h, site, clusters, s);
+        launch_split_fwd(mode, N.ln, false, F, sa, s);
+    } else {
+        launch_stream_fwd(mode, N.ln, a, s);
+    }
 }
+
+// The split form of the persistent Euler flow (euler_args' launch), or F = 1.
+int euler_split(const fqlpop* h, int nz) {
+    const NetLayout& N = h->bc;
+    if (!h->euler_fused || !split_fwd_supported(N.H, N.L, N.in_dim, N.out_dim, h->B)) return 1;
+    return split_factor(h, (long long)(h->B / 16) * nz, true);
+}
+SplitFwdArgs euler_split_args(fqlpop* h, const EulerArgs& ea, hipStream_t s) {
+    const NetLayout& N = h->bc;
+    SplitFwdArgs sa{};
+    StreamArgs& a = sa.s;
+    a.params = ea.params; a.P = ea.P; a.ens = 0;
+    for (int l = 0; l <= N.L; ++l) { a.w_off[l] = ea.w_off[l]; a.b_off[l] = ea.b_off[l]; }
+    a.x0 = ea.eu.p; a.x0_ss = ea.eu.ss; a.ld_x = ea.B; a.K0 = ea.D + ea.A + 1; a.L = ea.L; a.M = ea.B;
+    a.head.nout = ea.A;
+    a.ny = 1; a.nz = ea.nz; a.slots = ea.slots;
+    sa.aflow = ea.aflow;
+    sa.D = ea.D; sa.A = ea.A; sa.S = ea.S; sa.first = ea.first; sa.steps_f = ea.steps_f;
+    sa.probe = ea.probe;
+    sa.sync = split_prep(h, SITE_EULER, (long long)(ea.B / 16) * ea.nz, s);
+    return sa;
+}
+void launch_euler(fqlpop* h, const EulerArgs& ea, hipStream_t s) {
+    const int F = euler_split(h, ea.nz);
+    if (F > 1) launch_split_fwd(HEAD_EULER, false, true, F, euler_split_args(h, ea, s), s);
+    else launch_euler_flow(ea, s);
+}
+long long euler_blocks(const fqlpop* h, int nz) { return (long long)(h->B / 16) * nz * euler_split(h, nz); }
 
 // FQLPOP_SKIP (diagnostic builds only; TIMING EXPERIMENT, results are garbage): bit mask
 // of launches left out of the step, to measure each one's marginal cost in the concurrent
@@ -1042,37 +1098,36 @@ void euler_phase_report(const unsigned long long* ph, long long nb, int L, int s
 void flip_params(fqlpop* h);
 
 // Enqueue one population update (train) or one total_loss pass (!train).
+//
+// Capture rule (the HIP runtime's stream capture, ROCm 7.2): a side stream that waits on an
+// event joins the capture under the stream that recorded it, and hipStreamEndCapture resets
+// the joined streams recursively along those links.  A side stream that waited on another
+// side stream's event which itself (transitively) waited on the first would close a cycle
+// there and recurse without end (round 3's crash inside libamdhip64).  So the waits between
+// side streams form a chain: sF and sB fork from sM, sB waits on sF (the BC forward), and sF
+// never waits on sB; everything joins back into sM.
 void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     const Ctx c{h, h->nz};
     const int B = h->B, D = h->D, A = h->A, H = h->H, E = h->E, L = h->L, S = h->S;
     const int Kc = D + A, Kb = D + A + 1;
     const int B2 = 2 * B, B3 = 3 * B;
-    hipStream_t sM = h->sM, sF = h->sF, sB = h->sB, sX = h->sX;
+    hipStream_t sM = h->sM, sF = h->sF, sB = h->sB;
     h->ev_next = 0;
     h->probe_idx = 0;
     h->cr_in = h->cr_in_buf[h->cur];
-    const bool xin = train && h->xs_in, xout = train && h->xs_out;  // cross-step critic tail (fqlpop::xstep)
-    if (xin) {
-        // the previous step's critic partial fold + fused dW / optimiser on sB, with that step's
-        // parameter buffers (its closure reads them from h): first in the graph, no wait (the
-        // previous graph, which produced its operands, has completed)
-        ARGCHK(h->xs_tail[h->cur ^ 1], "cross-step tail: no deferred critic optimiser");
-        // sB joins the capture first (a launch on a stream outside the capture would run
-        // eagerly instead of becoming a node of this graph)
-        HIPCHK(hipEventRecord(h->ev_cdone, sM));
-        HIPCHK(hipStreamWaitEvent(sB, h->ev_cdone, 0));
-        flip_params(h);
-        h->skip_dw_wait = true;
-        h->xs_tail[h->cur]();
-        h->skip_dw_wait = false;
-        flip_params(h);
-        h->cr_in = h->cr_in_buf[h->cur];
-    }
     // the persistent Euler launch writes both stamps of every block it launches, and the
-    // reduction reads only those (probe_nz): no per-step clearing node at the step's head
+    // reduction reads only those (probe_nb): no per-step clearing node at the step's head
     if (h->probe_set >= 0 && !h->euler_fused)
         HIPCHK(hipMemsetAsync(h->probe_slots + 2LL * h->probe_blocks * h->probe_set * h->probe_pairs, 0,
                               sizeof(unsigned long long) * 2 * h->probe_blocks * h->probe_pairs, sM));
+
+    // Fork / join helper: `to` waits for everything enqueued on `from` so far.
+    auto dep = [&](hipStream_t from, hipStream_t to) {
+        if (from == to) return;
+        hipEvent_t ev = next_event(h);
+        HIPCHK(hipEventRecord(ev, from));
+        HIPCHK(hipStreamWaitEvent(to, ev, 0));
+    };
 
     // ---- sampling / assembly ------------------------------------------
     const auto& dset = (!train && h->ds[1].rows > 0) ? h->ds[1] : h->ds[0];
@@ -1082,7 +1137,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     sa.inj_batch = inj_batch ? h->inj_batch : nullptr;
     sa.inj_noise = inj_noise ? h->inj_noise : nullptr;
     sa.seeds = h->skeys; sa.count = h->count;
-    sa.step_add = xin ? 1 : 0;  // count is the previous step's until its finalize below
+    sa.step_add = 0;
     sa.stream_salt = train ? 0x51A7u : 0x5A1Du;
     sa.B = B; sa.D = D; sa.A = A;
     sa.os_in = tref(h->os_in, (long long)Kc * B3);
@@ -1095,33 +1150,10 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     sa.rew_t = tref(h->rew_t, B);
     sa.mask_t = tref(h->mask_t, B);
     sa.nz = c.nz; sa.slots = h->slots;
-    if (h->pipe_exp && train) {
-        // TIMING EXPERIMENT ONLY (results are racy): the next step's sampling, BC forward
-        // and flow wait only for the previous step's BC optimiser
-        if (h->pipe_started) HIPCHK(hipStreamWaitEvent(sF, h->pipe_exp == 2 ? h->ev_t1 : h->ev_bdone, 0));
-        launch_sample(sa, sF);
-        HIPCHK(hipEventRecord(h->ev_sample, sF));
-        HIPCHK(hipStreamWaitEvent(sM, h->ev_sample, 0));
-        HIPCHK(hipStreamWaitEvent(sB, h->ev_sample, 0));
-        h->pipe_started = true;
-    } else {
-        launch_sample(sa, sM);
-        HIPCHK(hipEventRecord(h->ev_sample, sM));
-        HIPCHK(hipStreamWaitEvent(sF, h->ev_sample, 0));
-        HIPCHK(hipStreamWaitEvent(sB, h->ev_sample, 0));
-    }
-    if (xin) {
-        // the previous step's finalize (grad stats, count += 1) after its critic optimiser and
-        // after this step's sampler read count
-        FinalArgs fa{};
-        fa.stats = h->stats; fa.chunk_leaf = h->chunk_leaf; fa.leaf_first = h->leaf_first;
-        fa.n_total_chunks = h->n_chunks_total; fa.n_leaves = h->n_train_leaves;
-        fa.info = tref(h->info, FQLPOP_INFO_STRIDE);
-        fa.count = h->count;
-        fa.nz = c.nz; fa.slots = h->slots;
-        launch_finalize(fa, sB);
-        HIPCHK(hipEventRecord(h->ev_cdone, sB));
-    }
+    launch_sample(sa, sM);
+    HIPCHK(hipEventRecord(h->ev_sample, sM));
+    if (sF != sM) HIPCHK(hipStreamWaitEvent(sF, h->ev_sample, 0));
+    if (sB != sM) HIPCHK(hipStreamWaitEvent(sB, h->ev_sample, 0));
 
     float* info = train ? h->info : h->vinfo;
     LossArgs la{};
@@ -1172,7 +1204,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             EulerArgs ea = euler_args(h, c.nz);
             if (h->probe_set >= 0 && h->probe_idx < h->probe_pairs)
                 ea.probe = h->probe_slots + 2 * h->probe_blocks * ((long long)h->probe_set * h->probe_pairs + h->probe_idx++);
-            if (!(skip_mask() & 1)) launch_euler_flow(ea, sF);
+            if (!(skip_mask() & 1)) launch_euler(h, ea, sF);
         }
         for (int i = 1; !h->euler_fused && i < S + (S == 1 ? 1 : 0); ++i) {
             // S == 1: one zero-cost pass that only clips (not used by the configs here)
@@ -1188,19 +1220,9 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         HIPCHK(hipEventRecord(h->ev_flow, sF));
     }
 
-    // Fork / join helper: `to` waits for everything enqueued on `from` so far.
-    auto dep = [&](hipStream_t from, hipStream_t to) {
-        hipEvent_t ev = next_event(h);
-        HIPCHK(hipEventRecord(ev, from));
-        HIPCHK(hipStreamWaitEvent(to, ev, 0));
-    };
-
     // ---- sB: BC loss + backward + Adam ------------------------------------
-    // (Adam writes params_nx, so it need not wait for the flow's reads).  Engine option
-    // bc_late: captured after the critic forward (1) or backward (2) of the main chain, whose
-    // completion it then waits for (schedule experiment)
-    auto bc_chain = [&]() {
-    HIPCHK(hipStreamWaitEvent(sB, h->ev_bcfwd, 0));
+    // (Adam writes params_nx, so it need not wait for the flow's reads)
+    if (sB != sF) HIPCHK(hipStreamWaitEvent(sB, h->ev_bcfwd, 0));
     launch_loss_bc(la, sB);
     HIPCHK(hipEventRecord(h->ev_bcloss, sB));
     if (train) {
@@ -1217,8 +1239,6 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         }
     }
     HIPCHK(hipEventRecord(h->ev_bdone, sB));
-    };
-    if (h->opt.bc_late == 0) bc_chain();
 
     // ---- sM: one-step actor forward on [s'; s; s] (z_next; z_d; z_metric) --
     {
@@ -1238,18 +1258,14 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             launch_head_fwd(HEAD_OS, ha, sM);
         }
     }
-    dep(sM, sX);  // a' is in the target-critic input
-    // cross-step tail: the previous step's critic optimiser (target EMA, critic params and
-    // W^T) and finalize (count) are done before this step's target critic and critic read them
-    if (xin) HIPCHK(hipStreamWaitEvent(sX, h->ev_cdone, 0));
     const NetLayout& NC = h->critic;
     const long long sy2 = (long long)H * B2, sy1 = (long long)H * B;
-    // ---- sX: target critic on [s', a'] (params from the target arena) -----
+    // ---- sM: target critic on [s', a'] (params from the target arena) -----
     if (h->stream_fwd) {
         HeadArgs ht{};
         ht.B = B; ht.D = D; ht.steps_f = (float)S;
         ht.o0 = tref(h->qt, (long long)E * B, B); ht.ld0 = B;
-        stream_fwd(c, sX, NC, h->target, h->PT, tref(h->tg_in, (long long)Kc * B), B, B, nullptr, nullptr, nullptr,
+        stream_fwd(c, sM, NC, h->target, h->PT, tref(h->tg_in, (long long)Kc * B), B, B, nullptr, nullptr, nullptr,
                    nullptr, 0, 0, 0, 0, 0, 0, HEAD_STORE, ht);
     } else {
         const NetLayout& N = NC;
@@ -1262,7 +1278,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             g.M = H; g.N = B; g.K = N.kdim(l);
             g.lda = H; g.ldb = B; g.ldc = B;
             g.ny = E; g.nz = c.nz; g.slots = h->slots;
-            gemm(LAYOUT_FWD, N.ln ? EPI_BIAS : EPI_BIAS_GELU, g, sX);
+            gemm(LAYOUT_FWD, N.ln ? EPI_BIAS : EPI_BIAS_GELU, g, sM);
             if (N.ln) {
                 LnArgs a{};
                 a.u = tref(h->tg_u[l], (long long)H * B * E, sy1);
@@ -1272,7 +1288,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
                 a.gamma = tref(h->target + N.gam[l], h->PT, N.ens_size);
                 a.beta = tref(h->target + N.bet[l], h->PT, N.ens_size);
                 a.H = H; a.M = B; a.ld = B; a.ny = E; a.nz = c.nz; a.slots = h->slots;
-                launch_ln_gelu_fwd(a, sX);
+                launch_ln_gelu_fwd(a, sM);
             }
         }
         HeadArgs ht{};
@@ -1282,26 +1298,13 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         ht.H = H; ht.M = B; ht.ld = B; ht.nout = 1; ht.B = B; ht.D = D; ht.steps_f = (float)S;
         ht.o0 = tref(h->qt, (long long)E * B, B); ht.ld0 = B;
         ht.ny = E; ht.nz = c.nz; ht.slots = h->slots;
-        launch_head_fwd(HEAD_STORE, ht, sX);
+        launch_head_fwd(HEAD_STORE, ht, sM);
     }
     // ---- sM: critic on [s,a ; s,clip(a_pi)] -------------------------------
-    // fuse_dq: the head writes the critic-loss gradient seeds dq (elementwise given Q_target,
-    // which precedes it on sM), so the critic backward follows the forward directly and
-    // loss_critic (info, head-bias grad sums) runs off the chain on sF
-    const bool fdq = train && h->opt.fuse_dq && h->stream_fwd && h->stream_bwd && !h->cfg.normalize_q_loss &&
-                     sX == sM && NC.out_dim == 1;
-    if (xin && sX != sM) HIPCHK(hipStreamWaitEvent(sM, h->ev_cdone, 0));
     {
         const NetLayout& N = NC;
         HeadArgs hc = head_args(c, N, h->cr_h[L - 1], B2, B2, sy2);
         hc.o0 = tref(h->q, (long long)E * B2, B2); hc.ld0 = B2;
-        if (fdq) {
-            hc.dq = la.dq; hc.qt = la.qt; hc.rew = la.rew; hc.mask = la.mask;
-            hc.discount = h->cfg.discount;
-            hc.inv_eb = 1.0f / (float)(E * B);
-            hc.gpi = -1.0f * hc.inv_eb;  // (normalize_q_loss off: lam = 1)
-            hc.q_min = h->cfg.q_agg_min; hc.E = E;
-        }
         if (h->stream_fwd) {
             // the a_pi columns [B, 2B) are back-propagated for dQ/da only: their layer outputs
             // (the dW GEMMs' operand) are not needed by the streamed backward
@@ -1314,35 +1317,13 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             launch_head_fwd(HEAD_STORE, hc, sM);
         }
     }
-    dep(sX, sM);  // Q_target
-    if (h->opt.bc_late == 1) {
-        dep(sM, sB);
-        bc_chain();
-    }
-    if (fdq) {
-        la.dq_fused = 1;
-        dep(sM, sF);  // after the critic forward (sF is idle after the flow)
-        launch_loss_critic(la, sF);
-        HIPCHK(hipEventRecord(h->ev_flow, sF));  // the actor loss reads its info[7]; the critic optimiser its head-bias grads
-    } else {
-        if (h->opt.early_join == 1) {
-            HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
-            HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
-        }
-        launch_loss_critic(la, sM);
-    }
-    if (h->opt.early_join == 2 && !fdq) {
-        // (the waits of the actor loss, moved ahead of the critic backward: a wait on a launch
-        // that finished long before resolves at once, while a wait on one that just finished
-        // on another queue costs that queue's signal latency, ~13 us in the step timeline)
-        HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
-        HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
-    }
-    // fused optimiser: the critic's dW + Adam is captured after the actor's dX
-    // chain (it runs beside it instead of ahead of it on a shared queue)
+    launch_loss_critic(la, sM);
+    // the fused optimiser: the critic's dW + Adam is captured after the actor's dX chain, on
+    // sB (idle by then), so that it runs beside that chain instead of ahead of it on a shared
+    // queue (+0.5-0.9 %)
     std::function<void()> critic_dw;
     if (train) {
-        // critic backward: the dX chain stays on sM, the dW GEMMs go to sX
+        // critic backward: the dX chain on sM
         InGradArgs ig{};
         ig.W0 = pref(h, h->params, NC, NC.W[0]);
         ig.du0 = tref(h->cr_du[0], (long long)H * B2 * E, sy2);
@@ -1352,69 +1333,49 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         if (h->stream_bwd) {
             stream_bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0),
                            B2, 0, B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, B2, h->part_cr,
-                           h->fused_adam && h->cdw_sb ? sB : sX, &ig, h->fused_adam ? &critic_dw : nullptr);
+                           h->fused_adam ? sB : sM, &ig, h->fused_adam ? &critic_dw : nullptr);
         } else {
             bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0), B2, 0,
                     B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, h->cr_dh, h->cr_c1, h->cr_c2,
-                    B2, sX);
+                    B2, sM);
             launch_input_grad(ig, sM);
         }
-        // critic Adam + target EMA; the per-layer backward writes grads on sM too: join it
+        // critic Adam + target EMA (the unfused paths)
         if (!h->fused_adam) {
-            dep(sM, sX);
-            adam_net(c, sX, 0);
-            if (h->stream_bwd) transpose_nets(h, sX, 1, false, h->params_nx, h->paramsT_nx);
+            adam_net(c, sM, 0);
+            if (h->stream_bwd) transpose_nets(h, sM, 1, false, h->params_nx, h->paramsT_nx);
         }
     }
-    if (h->opt.bc_late == 2) {
-        dep(sM, sB);
-        bc_chain();
-    }
-    HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
-    HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
+    if (sF != sM) HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
+    if (sB != sM) HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
     launch_loss_actor(la, sM);
-    if (h->pipe_exp == 2 && train) HIPCHK(hipEventRecord(h->ev_t1, sM));
     if (train) {
         const NetLayout& N = h->os;
         if (h->fused_adam) {
             // the critic's dW launch waits for the actor loss too, so that the actor backward
             // (the critical chain) is dispatched first: a dW launch dispatched ahead of it
             // takes every CU's LDS (3 blocks of 51 KB) and starves it
-            dep(sM, h->cdw_sb ? sB : sX);
-            // actor dX chain, then the critic's grads + Adam (sX) beside the
-            // actor's (sM), then the join
+            dep(sM, sB);
+            // actor dX chain, then the critic's grads + Adam (sB) beside the actor's (sM), then
+            // the join
             std::function<void()> os_dw;
             stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3,
                            B, B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, B, h->part_os, sM, nullptr,
                            &os_dw);
-            if (xout) {
-                h->xs_tail[h->cur] = critic_dw;  // (the next step's graph runs it)
-            } else {
-                if (fdq) HIPCHK(hipStreamWaitEvent(h->cdw_sb ? sB : sX, h->ev_flow, 0));  // g_cb4 (loss_critic)
-                critic_dw();  // the fused launches include each net's small-leaf Adam
-            }
+            critic_dw();  // the fused launches include each net's small-leaf Adam
             os_dw();
-            if (xout) {
-                // this step's finalize runs in the next step's graph too: join the streams
-                dep(sB, sM);
-                HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
-                HIPCHK(hipGetLastError());
-                return;
-            }
-            if (h->cdw_sb) dep(sB, sM);
-        } else if (h->stream_bwd)
-            stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3,
-                           B, B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, B, h->part_os, sX);
-        else
-            bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3, B, B,
-                    B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, h->os_dh, nullptr, nullptr, B, sX);
-        if (!h->fused_adam) {
-            dep(sM, sX);
-            adam_net(c, sX, 2);
-            if (h->stream_bwd) transpose_nets(h, sX, 4, false, h->params_nx, h->paramsT_nx);
+            dep(sB, sM);
+        } else {
+            if (h->stream_bwd)
+                stream_bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3),
+                               B3, B, B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, B, h->part_os, sM);
+            else
+                bwd_net(c, sM, N, tref(h->dout_os, (long long)A * B), B, tref(h->os_in + B, (long long)Kc * B3), B3, B,
+                        B, B, h->os_u, h->os_g, 0, nullptr, nullptr, 0, h->os_du, h->os_dh, nullptr, nullptr, B, sM);
+            adam_net(c, sM, 2);
+            if (h->stream_bwd) transpose_nets(h, sM, 4, false, h->params_nx, h->paramsT_nx);
         }
-        dep(sX, sM);
-        HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
+        if (sB != sM) HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
         FinalArgs fa{};
         fa.stats = h->stats; fa.chunk_leaf = h->chunk_leaf; fa.leaf_first = h->leaf_first;
         fa.n_total_chunks = h->n_chunks_total; fa.n_leaves = h->n_train_leaves;
@@ -1422,7 +1383,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         fa.count = h->count;
         fa.nz = c.nz; fa.slots = h->slots;
         launch_finalize(fa, sM);
-    } else {
+    } else if (sB != sM) {
         HIPCHK(hipStreamWaitEvent(sM, h->ev_bdone, 0));
     }
     HIPCHK(hipGetLastError());
@@ -1456,14 +1417,13 @@ void run(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     if (train) flip_params(h);
 }
 
-// The graph of one step for the current (mode, active count, probe set, parameter buffer,
-// cross-step flags), captured if missing (or always, with `recapture`).
+// The graph of one step for the current (mode, active count, probe set, parameter buffer),
+// captured if missing (or always, with `recapture`).
 Graphs& graph_for(fqlpop* h, bool train, bool inj_batch, bool inj_noise, bool recapture) {
     // one graph per (mode, active-member count): kernels read the active slot ids
     // from device memory, so any active set of the same size replays the graph
     const long long key = ((train ? 4 : 0) + (inj_batch ? 2 : 0) + (inj_noise ? 1 : 0)) + 8LL * h->nz +
-                          (1LL << 32) * (h->probe_set + 1) + (1LL << 36) * h->cur +
-                          (1LL << 38) * ((h->xs_in ? 1 : 0) + (h->xs_out ? 2 : 0));
+                          (1LL << 32) * (h->probe_set + 1) + (1LL << 36) * h->cur;
     Graphs& gr = h->graphs[key];
     if (recapture || gr.exec == nullptr || gr.nz != h->nz) {
         if (gr.exec) HIPCHK(hipGraphExecDestroy(gr.exec));
@@ -1485,35 +1445,6 @@ Graphs& graph_for(fqlpop* h, bool train, bool inj_batch, bool inj_noise, bool re
     return gr;
 }
 
-// Cross-step tail (fqlpop::xstep): capture every step graph variant a multi-step
-// fqlpop_step call uses, for both parameter buffers and (probe on) both probe sets, in an
-// order where each xs_in capture finds the deferred critic dW half of the other buffer's
-// xs_out capture of the same active count.  Once per active count (and after a parameter
-// upload); so that no graph is captured inside a caller's timed loop.
-void xs_prebuild(fqlpop* h) {
-    const long long tag = (long long)h->nz * 2 + (h->probe_set >= 0 ? 1 : 0);  // (both probe sets)
-    if (h->xs_built.count(tag)) return;
-    const int set0 = h->probe_set, cur0 = h->cur;
-    const bool in0 = h->xs_in, out0 = h->xs_out;
-    // (parity offset from cur0, xs_in, xs_out)
-    const int order[8][3] = {{0, 0, 1}, {1, 1, 1}, {0, 1, 1}, {1, 0, 1}, {0, 1, 0}, {1, 1, 0}, {0, 0, 0}, {1, 0, 0}};
-    for (int ps = 0; ps < (set0 >= 0 ? 2 : 1); ++ps) {
-        h->probe_set = set0 >= 0 ? set0 ^ ps : -1;
-        for (const auto& o : order) {
-            if ((h->cur ^ cur0) != o[0]) flip_params(h);
-            h->xs_in = o[1] != 0;
-            h->xs_out = o[2] != 0;
-            (void)graph_for(h, true, false, false, true);
-        }
-    }
-    if (h->cur != cur0) flip_params(h);
-    h->probe_set = set0;
-    h->xs_in = in0;
-    h->xs_out = out0;
-    h->xs_built.insert(tag);
-}
-
-
 // Launch duration from per-block stamps: max(end) - min(start) over the blocks
 // that ran (0 = slot not written).  s_memrealtime counts at 100 MHz.
 double probe_launch_us(const unsigned long long* v, long long blocks) {
@@ -1533,7 +1464,7 @@ void probe_consume(fqlpop* h, int set) {
     std::vector<unsigned long long> v(per * h->probe_pairs);
     std::memcpy(v.data(), h->probe_host + per * set * h->probe_pairs, sizeof(unsigned long long) * v.size());
     for (int p = 0; p < h->probe_pairs; ++p) {
-        const long long nb = h->euler_fused ? h->probe_blocks / h->n * h->probe_nz[set] : h->probe_blocks;
+        const long long nb = h->euler_fused ? h->probe_nb[set] : h->probe_blocks;
         const double us = probe_launch_us(v.data() + per * p, nb);
         if (us < 0) continue;  // launch not probed
         h->probe_total_ms += us * 1e-3;
@@ -1563,6 +1494,19 @@ int guard(F&& f) {
     } catch (const std::exception& e) {
         g_err = e.what();
         return FQLPOP_E_STATE;
+    }
+}
+
+// A split launch whose hand-off wait gave up (kernels.hip, sp_wait) left invalid results:
+// report it (once) instead of returning them.  The caller has synchronised the streams.
+void check_split_error(fqlpop* h) {
+    if (!h->split_err) return;
+    unsigned e = 0;
+    HIPCHK(hipMemcpy(&e, h->split_err, sizeof(e), hipMemcpyDeviceToHost));
+    if (e != 0) {
+        HIPCHK(hipMemset(h->split_err, 0, sizeof(e)));
+        throw FqErr{FQLPOP_E_STATE, "a split launch's hand-off wait timed out (blocks of a cluster not resident "
+                                    "together); results of the last steps are invalid"};
     }
 }
 
@@ -1667,50 +1611,24 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
 
         h->opt = g_engine_opts;
         const EngineOptions& eo = h->opt;
-        // Stream priorities (engine option prio): 0 = all default (measured fastest),
-        // 1 = main chain high, 2 = Euler flow high.
-        {
-            int least = 0, greatest = 0;
-            HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-            HIPCHK(hipStreamCreateWithPriority(&h->sM, hipStreamNonBlocking, eo.prio == 1 ? greatest : 0));
-            HIPCHK(hipStreamCreateWithPriority(&h->sF, hipStreamNonBlocking, eo.prio == 2 ? greatest : 0));
-            HIPCHK(hipStreamCreateWithPriority(&h->sB, hipStreamNonBlocking, eo.prio == 1 ? least : 0));
-        }
-        // A 4th stream (target critic + dW GEMMs + Adams off the main chain) is
-        // opt-in: on MI355X the step is throughput-bound and the extra
-        // concurrency measured 5% slower.
-        if (eo.streams >= 4) HIPCHK(hipStreamCreateWithFlags(&h->sX, hipStreamNonBlocking));
-        else h->sX = h->sM;
-        // serial (profiling option): every kernel of the step on sM, so a kernel trace
-        // shows uncontended durations
+        // three streams; serial (profiling option): every kernel of the
+        // step on sM, so a kernel trace shows uncontended durations
+        HIPCHK(hipStreamCreateWithFlags(&h->sM, hipStreamNonBlocking));
         if (eo.serial) {
-            HIPCHK(hipStreamDestroy(h->sF));
-            HIPCHK(hipStreamDestroy(h->sB));
-            if (h->sX != h->sM) HIPCHK(hipStreamDestroy(h->sX));
-            h->sF = h->sB = h->sX = h->sM;
+            h->sF = h->sB = h->sM;
+        } else {
+            HIPCHK(hipStreamCreateWithFlags(&h->sF, hipStreamNonBlocking));
+            HIPCHK(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
         }
         h->ev_pool.resize(64);
-        {
-            // FQLPOP_PIPE_EXP (diagnostic builds only; eager launches, racy): the next step's
-            // sampling / BC forward / flow start before the previous step has finished
-            const char* pe = diag_env("FQLPOP_PIPE_EXP");
-            h->pipe_exp = pe && !cfg->use_graph ? std::atoi(pe) : 0;
-        }
         h->euler_fused = euler_flow_supported(H, L, D, A, B) && !h->bc.ln && eo.euler_fused;
         h->stream_fwd = stream_fwd_supported(H, L, D + A + 1, A, B) && eo.stream_fwd;
         h->stream_bwd = stream_bwd_supported(H, L, A, B, B) && eo.stream_bwd;
-        // the critic's fused dW + optimiser on the BC stream (idle by then), beside the
-        // actor chain: +0.5-0.9 % (cdw_sb = 0: on the main chain's queue)
-        h->cdw_sb = eo.cdw_sb != 0;
         // Adam / EMA / W^T / grad stats fused into the grouped dW epilogue
         h->fused_adam = h->stream_bwd && H % 128 == 0 && L <= GEMM_GROUP_MAX && h->critic.off == 0 && eo.fused_adam;
-        // cross-step critic tail: the graph path of the default schedule only (fused Euler,
-        // streamed backward, fused optimiser with the critic's on sB, three streams)
-        h->xstep = eo.xstep != 0 && cfg->use_graph && h->euler_fused && h->stream_bwd && h->fused_adam &&
-                   h->cdw_sb && eo.streams == 3 && !eo.serial;
         if (h->euler_fused) {  // dominant kernel: one persistent Euler launch per step
             h->probe_pairs = 1;
-            h->probe_blocks = (long long)(cfg->batch_size / 16) * n_members;
+            h->probe_blocks = std::max<long long>((long long)(cfg->batch_size / 16) * n_members, kSplitMaxBlocks);
         } else {               // dominant kernel: the Euler hidden-layer GEMMs
             h->probe_pairs = std::max(1, (cfg->flow_steps - 1) * (cfg->num_hidden - 1));
             h->probe_blocks = (long long)((cfg->hidden_dim + 63) / 64) * ((cfg->batch_size + 63) / 64) * n_members;
@@ -1741,7 +1659,7 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         for (auto& e : h->probe_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHK(hipStreamCreateWithFlags(&h->probe_stream, hipStreamNonBlocking));
         for (auto& e : h->ev_pool) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        for (hipEvent_t* e : {&h->ev_sample, &h->ev_bcfwd, &h->ev_bcloss, &h->ev_flow, &h->ev_bdone, &h->ev_cdone})
+        for (hipEvent_t* e : {&h->ev_sample, &h->ev_bcfwd, &h->ev_bcloss, &h->ev_flow, &h->ev_bdone})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         HIPCHK(hipEventCreate(&h->ev_t0));
         HIPCHK(hipEventCreate(&h->ev_t1));
@@ -1803,6 +1721,21 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             h->paramsT_buf[0] = h->paramsT = h->alloc(std::max<long long>(1, h->PTT));
             h->paramsT_buf[1] = h->paramsT_nx = h->alloc(std::max<long long>(1, h->PTT));
         }
+        // split launch sites: exchange and counters for up to kSplitMaxClusters tiles each
+        h->split_ok = h->stream_fwd && eo.split != 0;
+        if (h->split_ok) {
+            const long long tiles_per_member[SITE_N] = {B2 / 16, B / 16, B3 / 16, (long long)E * B / 16,
+                                                        (long long)E * B2 / 16};
+            for (int si = 0; si < SITE_N; ++si) {
+                auto& st = h->split_site[si];
+                st.clusters = std::min(kSplitMaxClusters, tiles_per_member[si] * n);
+                HIPCHK(hipMalloc(&st.xch, sizeof(float) * split_cluster_floats() * st.clusters));
+                HIPCHK(hipMalloc(&st.cnt, sizeof(unsigned) * split_counter_stride() * st.clusters));
+                HIPCHK(hipMemset(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * st.clusters));
+            }
+            HIPCHK(hipMalloc(&h->split_err, 64));
+            HIPCHK(hipMemset(h->split_err, 0, 64));
+        }
         h->cr_dh = h->alloc((long long)H * B2 * E);
         h->bc_dh = h->alloc((long long)H * B);
         h->os_dh = h->alloc((long long)H * B);
@@ -1852,7 +1785,12 @@ int fqlpop_destroy(fqlpop_t* h) {
         for (auto& d : h->ds)
             for (float* p : {d.obs, d.act, d.rew, d.mask, d.nobs})
                 if (p) (void)hipFree(p);
-        for (hipEvent_t e : {h->ev_sample, h->ev_bcfwd, h->ev_bcloss, h->ev_flow, h->ev_bdone, h->ev_cdone, h->ev_t0, h->ev_t1})
+        for (auto& st : h->split_site) {
+            if (st.xch) (void)hipFree(st.xch);
+            if (st.cnt) (void)hipFree(st.cnt);
+        }
+        if (h->split_err) (void)hipFree(h->split_err);
+        for (hipEvent_t e : {h->ev_sample, h->ev_bcfwd, h->ev_bcloss, h->ev_flow, h->ev_bdone, h->ev_t0, h->ev_t1})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
         for (hipEvent_t e : h->probe_done)
@@ -1876,7 +1814,6 @@ int fqlpop_destroy(fqlpop_t* h) {
             euler_phase_report(h->ephase_host, h->ephase_blocks, h->L, h->S - 1);
             (void)hipHostFree(h->ephase_host);
         }
-        if (h->sX && h->sX != h->sM) (void)hipStreamDestroy(h->sX);
         if (h->sF && h->sF != h->sM) (void)hipStreamDestroy(h->sF);
         if (h->sB && h->sB != h->sM) (void)hipStreamDestroy(h->sB);
         if (h->sM) (void)hipStreamDestroy(h->sM);
@@ -1910,7 +1847,6 @@ int fqlpop_set_dataset(fqlpop_t* h, int which, const float* obs, const float* ac
         // graphs bake dataset pointers in: drop them
         for (auto& kv : h->graphs)
             if (kv.second.exec) { HIPCHK(hipGraphExecDestroy(kv.second.exec)); kv.second.exec = nullptr; }
-        h->xs_built.clear();
     });
 }
 
@@ -1933,28 +1869,18 @@ int fqlpop_step(fqlpop_t* h, int n_steps) {
         ARGCHK(n_steps >= 0, "n_steps must be >= 0");
         if (h->ds[0].rows == 0) throw FqErr{FQLPOP_E_STATE, "no training dataset set (fqlpop_set_dataset)"};
         HIPCHK(hipSetDevice(h->device));
-        struct XsReset {  // (also on an exception)
-            fqlpop* h;
-            ~XsReset() { h->xs_in = h->xs_out = false; }
-        } xs_reset{h};
-        const bool xs = h->xstep && n_steps >= 2 && h->nz > 0;
         for (int i = 0; i < n_steps; ++i) {
-            // cross-step tail: every step but the last defers its critic optimiser to the next
-            h->xs_in = xs && i > 0;
-            h->xs_out = xs && i < n_steps - 1;
             if (h->probe) {
                 const int set = (int)(h->probe_step & 1);
                 if (h->probe_pending[set]) probe_consume(h, set);  // the step i-2 that used this set
                 h->probe_set = set;
-                h->probe_nz[set] = h->nz;
-                if (xs) xs_prebuild(h);
+                h->probe_nb[set] = euler_blocks(h, h->nz);
                 run(h, true, false, false);
                 h->probe_set = -1;
                 HIPCHK(hipEventRecord(h->probe_done[set], h->sM));
                 h->probe_pending[set] = true;
                 ++h->probe_step;
             } else {
-                if (xs) xs_prebuild(h);
                 run(h, true, false, false);
             }
         }
@@ -1998,6 +1924,7 @@ int fqlpop_read_info(fqlpop_t* h, int which, float* out) {
         ARGCHK(h && out, "null argument");
         HIPCHK(hipSetDevice(h->device));
         HIPCHK(hipStreamSynchronize(h->sM));
+        check_split_error(h);
         HIPCHK(hipMemcpy(out, which ? h->vinfo : h->info, sizeof(float) * FQLPOP_INFO_STRIDE * h->n,
                          hipMemcpyDeviceToHost));
     });
@@ -2197,7 +2124,7 @@ int fqlpop_sync(fqlpop_t* h) {
         HIPCHK(hipStreamSynchronize(h->sM));
         HIPCHK(hipStreamSynchronize(h->sF));
         HIPCHK(hipStreamSynchronize(h->sB));
-        if (h->sX != h->sM) HIPCHK(hipStreamSynchronize(h->sX));
+        check_split_error(h);
     });
 }
 
@@ -2222,7 +2149,7 @@ int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* 
         auto launch = [&](unsigned long long* probe) {
             if (h->euler_fused) {
                 ea.probe = probe;
-                launch_euler_flow(ea, h->sF);
+                launch_euler(h, ea, h->sF);
             } else {
                 g.probe = probe;
                 launch_gemm_euler_hidden(g, h->sF);
@@ -2248,7 +2175,7 @@ int fqlpop_time_dominant_kernel(fqlpop_t* h, int iters, double* avg_us, double* 
         std::vector<unsigned long long> v(2 * h->probe_blocks);
         std::memcpy(v.data(), h->probe_host, sizeof(unsigned long long) * v.size());
         h->clock_check_event_us = 1000.0 * ms;
-        h->clock_check_stamp_us = probe_launch_us(v.data(), h->probe_blocks);
+        h->clock_check_stamp_us = probe_launch_us(v.data(), h->euler_fused ? euler_blocks(h, h->nz) : h->probe_blocks);
     });
 }
 
@@ -2258,7 +2185,8 @@ int fqlpop_dominant_kernel_info(fqlpop_t* h, char* name, int name_cap, double* f
         const double B = h->B, H = h->H, K0 = h->D + h->A + 1, A = h->A, L = h->L, nz = h->nz;
         std::string nm;
         if (h->euler_fused) {
-            nm = "euler_flow_kernel";
+            const int F = euler_split(h, h->nz);
+            nm = F > 1 ? "split_fwd_kernel<HEAD_EULER> F=" + std::to_string(F) : "euler_flow_kernel";
             // unique bytes: the bc net's Dense kernels + biases, the state in, a_flow out
             *bytes = 4.0 * nz * (K0 * H + (L - 1) * H * H + H * A + L * H + A + K0 * B + A * B);
         } else {

@@ -3,7 +3,7 @@ batches, noise and initial parameters, called through the C ABI.
 
 Tolerance (north_star): per-step losses / Q statistics within 1e-4 relative
 (with an absolute floor of 1e-6 for values near zero).  After every step:
-Adam moments m and v of every leaf within 5e-4 of the leaf's scale (every gradient
+Adam moments m and v of every leaf within 2.5e-4 of the leaf's scale (every gradient
 element), and the optimiser step of every leaf exact against optax.adam / the EMA
 applied to the GPU's own previous state (tests/_helpers.OptimiserChecker).
 """
@@ -357,16 +357,22 @@ def _synthetic_rows(N, D, A, seed):
             "next_observations": (obs + 0.05 * rng.standard_normal((N, D))).astype(np.float32)}
 
 
-@pytest.mark.parametrize("D,A,B,alphas,kw", [
-    (28, 5, 256, [10.0, 216.8], {}),                  # BASELINE C2 shapes (cube)
-    (42, 8, 1024, [31.6], dict(discount=0.995)),      # BASELINE C3 shapes (antsoccer)
+_C2_ALPHAS = np.logspace(np.log10(3), np.log10(1000), 16).tolist()   # bench.py / tune_alpha.py:43-45
+
+
+@pytest.mark.parametrize("D,A,B,alphas,steps,kw", [
+    (28, 5, 256, [10.0, 216.8], 3, {}),               # C2 shapes, 2 members: the split launches (auto)
+    (28, 5, 256, _C2_ALPHAS, 2, {}),                  # BASELINE C2: the benchmarked 16-member population
+    (42, 8, 1024, [31.6], 3, dict(discount=0.995)),   # BASELINE C3 shapes (antsoccer)
+    (42, 8, 1024, _C2_ALPHAS[::4], 2, dict(discount=0.995)),  # C3, 4 members
 ])
-def test_production_step_matches_oracle_on_its_own_draws(D, A, B, alphas, kw):
+def test_production_step_matches_oracle_on_its_own_draws(D, A, B, alphas, steps, kw):
     """fqlpop_step -- the path Trainer and bench.py run -- against the oracle: the device
     sampler's rows, flow times and noises are reproduced on the host (tests/philox_np.py,
     Philox4x32-10 pinned to the Random123 known answers), the oracle updates on
-    dataset[idx] with those noises, and all 13 info values must agree to 1e-4 at every
-    one of 3 steps, and so must every leaf's Adam moments and optimiser step."""
+    dataset[idx] with those noises, and all 13 info values of EVERY member (slot-dependent
+    indexing: the 16-member case covers slots 0-15, two members per XCD) must agree to 1e-4
+    at every step, and so must every leaf's Adam moments and optimiser step."""
     from fqlpop import Population, PopulationConfig
     from philox_np import draw, sample_key
     H, N = 512, 100_003
@@ -383,7 +389,7 @@ def test_production_step_matches_oracle_on_its_own_draws(D, A, B, alphas, kw):
     keys = [sample_key(int(pop.seeds[i]), float(pop.alphas[i])) for i in range(len(alphas))]
     d64 = O.cast_tree(data, np.float64)
     checks = [OptimiserChecker(pop, i, ocfgs[i].lr, ocfgs[i].tau) for i in range(len(alphas))]
-    for step in range(3):
+    for step in range(steps):
         for c in checks:
             c.before()
         pop.step(1)
@@ -431,47 +437,3 @@ def test_device_init_properties():
         assert pop.get_count(i) == 0
         assert not np.any(pop.get_flat(i, STATE_ADAM_M)) and not np.any(pop.get_flat(i, STATE_ADAM_V))
     pop.close()
-
-
-@pytest.mark.parametrize("calls", [[7], [5, 1, 9, 2]])
-def test_cross_step_tail_bit_identical(calls):
-    """Engine option xstep: inside one step() call every step's critic dW / optimiser and
-    grad-stat finalize run at the head of the next step's graph (sampler reads count + 1
-    ahead of that finalize; cr_in per parameter buffer).  Several calls, one of a single
-    step, give the same parameters, Adam state, target, info and counts as the default
-    schedule, and the in-step probe times every step's Euler launch once."""
-    steps = sum(calls)
-    with engine_options():
-        ref = _sampled_run_now(512, 256, steps, calls, probe=True)
-    with engine_options(xstep=1):
-        got = _sampled_run_now(512, 256, steps, calls, probe=True)
-    assert np.array_equal(got[0], ref[0])
-    for a, b in zip(got[1], ref[1]):
-        assert np.array_equal(a, b)
-    assert got[3] == ref[3] == [steps] * 3
-    assert got[2][1] == ref[2][1] == steps, (got[2], ref[2])
-
-
-@pytest.mark.parametrize("opt", [{"bc_late": 1}, {"bc_late": 2}, {"early_join": 1}, {"early_join": 2}])
-def test_schedule_options_bit_identical(opt):
-    """Engine options bc_late (the BC update captured after the critic forward / backward) and
-    early_join (the main chain's waits for the flow / BC loss moved ahead) only move launches
-    or edges in the step's DAG: the same parameters, Adam state, target and info."""
-    ref = _sampled_run(512, 256, 3, {})
-    got = _sampled_run(512, 256, 3, opt)
-    assert np.array_equal(got[0], ref[0])
-    for a, b in zip(got[1], ref[1]):
-        assert np.array_equal(a, b)
-
-
-def test_fused_critic_loss_seeds_match_loss_kernel():
-    """Engine option fuse_dq (off: measured 1.1 % slower): the critic forward's head writes the critic-loss
-    gradient seeds and loss_critic runs off the chain.  Same arithmetic as loss_critic's
-    seeds: parameters, Adam state, target and info agree with fuse_dq = 0 after 3
-    device-sampled steps (bit-identical unless the two kernels contract the target's
-    r + gamma mask agg differently; then within 1e-6 relative)."""
-    ref = _sampled_run(512, 256, 3, {})
-    got = _sampled_run(512, 256, 3, {"fuse_dq": 1})
-    np.testing.assert_allclose(got[0], ref[0], rtol=1e-6, atol=1e-7)
-    for a, b in zip(got[1], ref[1]):
-        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)

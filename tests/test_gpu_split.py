@@ -1,0 +1,89 @@
+"""Split launches (engine option ``split``; kernels.hip, "split streamed forward"): small
+populations run the streamed forwards and the Euler flow as clusters of 2, 4 or 8 blocks
+per 16-column tile that hand every hidden layer's output to each other through L2 / MALL.
+
+Each output element keeps the unsplit fp32 chain (full K in the unsplit k order, the
+LayerNorm and head partials summed in the unsplit order), so a split run must be
+BIT-IDENTICAL to the unsplit one: parameters, Adam moments, target critic, info and val
+info after several device-sampled steps, for every split factor and member count.  That
+is also what keeps a member's results independent of how many members share its GPU (the
+world size of a sharded population).  Oracle parity of the split path itself: the 2-member
+production-step test of test_gpu_parity.py runs on it (auto split)."""
+import numpy as np
+import pytest
+
+from _helpers import engine_options
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(N, D, A, seed):
+    rng = np.random.default_rng(seed)
+    obs = rng.standard_normal((N, D)).astype(np.float32)
+    rew = np.where(rng.uniform(size=N) < 0.05, 0.0, -1.0).astype(np.float32)
+    return {"observations": obs, "actions": rng.uniform(-1 + 1e-5, 1 - 1e-5, (N, A)).astype(np.float32),
+            "rewards": rew, "masks": (1.0 - (rew == 0)).astype(np.float32),
+            "next_observations": (obs + 0.05 * rng.standard_normal((N, D))).astype(np.float32)}
+
+
+def _run(opts, n_members, D=28, A=5, B=256, steps=3, **kw):
+    from fqlpop import Population, PopulationConfig
+    alphas = [3.0 * 3.3 ** i for i in range(n_members)]
+    with engine_options(**opts):
+        pop = Population(PopulationConfig(obs_dim=D, action_dim=A, hidden_dims=(512,) * 4, batch_size=B, **kw),
+                         alphas, [11 + i for i in range(n_members)])
+        pop.set_dataset(_data(20_000, D, A, 3))
+        pop.step(steps)
+        info = pop.read_info_array().copy()
+        rng = np.random.default_rng(9)
+        val = {"observations": rng.standard_normal((B, D)).astype(np.float32),
+               "actions": rng.uniform(-1, 1, (B, A)).astype(np.float32),
+               "rewards": -np.ones(B, np.float32), "masks": np.ones(B, np.float32),
+               "next_observations": rng.standard_normal((B, D)).astype(np.float32)}
+        pop.total_loss([val] * n_members)
+        vinfo = pop.read_info_array("val").copy()
+        flats = [pop.get_flat(i, w) for i in range(n_members) for w in (0, 1, 2)]
+        name = pop.dominant_kernel_info()[0]
+        pop.close()
+    return info, vinfo, flats, name
+
+
+def _same(a, b):
+    assert np.array_equal(a[0], b[0]), "train info differs"
+    assert np.array_equal(a[1], b[1]), "val info differs"
+    for i, (x, y) in enumerate(zip(a[2], b[2])):
+        assert np.array_equal(x, y), f"state {i} differs (max |d| {np.abs(x - y).max()})"
+
+
+@pytest.mark.parametrize("n,F", [(1, 8), (2, 8), (2, 4), (2, 2), (3, 4)])
+def test_split_bit_identical_to_unsplit_cube(n, F):
+    ref = _run({"split": 0}, n)
+    got = _run({"split": F}, n)
+    assert got[3].startswith("split_fwd_kernel"), got[3]
+    assert ref[3] == "euler_flow_kernel"
+    _same(got, ref)
+
+
+def test_split_auto_bit_identical_antsoccer_shape():
+    """BASELINE C3 shapes (obs 42, act 8, B = 1024), one member: auto splits the Euler
+    flow (64 tiles x 4 blocks), the BC forward and the target critic (128 tiles x 2); the
+    one-step and critic forwards (192, 256 tiles) stay unsplit."""
+    ref = _run({"split": 0}, 1, D=42, A=8, B=1024, steps=2, discount=0.995)
+    got = _run({}, 1, D=42, A=8, B=1024, steps=2, discount=0.995)
+    _same(got, ref)
+
+
+def test_split_no_error_word_and_probe_times_split_launch():
+    """The in-step probe times the split Euler launch (every block's stamps), and no
+    hand-off wait gave up (the runtime raises on the error word at sync)."""
+    from fqlpop import Population, PopulationConfig
+    pop = Population(PopulationConfig(hidden_dims=(512,) * 4, batch_size=256), [3.0, 30.0], [1, 2])
+    pop.set_dataset(_data(20_000, 28, 5, 4))
+    pop.set_probe(True)
+    pop.step(6)
+    pop.sync()
+    us, n, _ = pop.read_probe()
+    assert n == 6 and us > 0
+    name = pop.dominant_kernel_info()[0]
+    assert name.startswith("split_fwd_kernel"), name
+    pop.close()
