@@ -264,6 +264,11 @@ void launch_stream_bwd(bool ln, const StreamBwdArgs& a, hipStream_t s);
 //   then H*nout head kernel W_L[k][j] at k*nout + j.
 inline int stream_bwd_np(int L, int H, int nout, bool ln) { return (ln ? 3 : 1) * L * H + H * nout; }
 
+// Split form of launch_stream_bwd for small populations (F = 8, 4 or 2 blocks per 16-column
+// tile, bit-identical; the SplitSync of the launch site, counters zeroed before the launch).
+bool split_bwd_supported(int H, int L, int nout, int M, int Mg);
+void launch_split_bwd(bool ln, int F, const StreamBwdArgs& a, const SplitSync& sy, hipStream_t s);
+
 struct ColsumArgs {                      // grads[off(p)] = sum over tiles of part[t][p]
     const float* part;
     int NP, tiles;                        // tiles that hold partials (Mg / 16)

@@ -1013,6 +1013,43 @@ DEV float gelu_grad_fast(float x) {
     return fmaf(sg, x * (1.0f - sg) * fmaf(x2, kD1, kD0), sg);
 }
 
+// LayerNorm arithmetic with every rounding explicit (fp contraction off, fmaf where a
+// fused multiply-add is meant), so that the unsplit and the split kernels, whose code around
+// these sums differs, give bit-identical results.
+DEV void ln_acc(float v, float& s1, float& s2) {  // column sums of x and x^2
+#pragma clang fp contract(off)
+    s1 = s1 + v;
+    s2 = fmaf(v, v, s2);
+}
+DEV void ln_stats(float S1, float S2, float h, float& mean, float& rs) {  // from the feature sums
+#pragma clang fp contract(off)
+    mean = S1 / h;
+    const float var = fmaxf(fmaf(-mean, mean, S2 / h), 0.f);
+    rs = 1.0f / sqrtf(var + 1e-6f);
+}
+DEV float ln_apply(float v, float mean, float rs, float ga, float be) {
+#pragma clang fp contract(off)
+    return fmaf((v - mean) * rs, ga, be);
+}
+// backward: d = dh gamma (rounded), its column sums s1 += d, s2 += d xhat
+DEV float ln_bwd_acc(float dh, float gm, float xh, float& s1, float& s2) {
+#pragma clang fp contract(off)
+    const float d = dh * gm;
+    s1 = s1 + d;
+    s2 = fmaf(d, xh, s2);
+    return d;
+}
+// du = rstd (d - c1 - xhat c2) gelu'(u)
+DEV float ln_bwd_du(float d, float xh, float c1, float c2, float rs, float gp) {
+#pragma clang fp contract(off)
+    return (rs * fmaf(-xh, c2, d - c1)) * gp;
+}
+// one product rounded on its own, then summed (LN scale grads: sum over columns of dh xhat)
+DEV float mul_rn(float a, float b) {
+#pragma clang fp contract(off)
+    return a * b;
+}
+
 // One streamed layer's k-loop: acc[c] += W[k][64w + 4li + c] * xs[k][li] over
 // k < 4 NS (NS a multiple of EF_PF).  ring[] holds the next EF_PF k-steps' A
 // fragments on entry; on exit it holds the first EF_PF of the layer at
@@ -1502,10 +1539,7 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    s1 += v[r][c];
-                    s2 += v[r][c] * v[r][c];
-                }
+                for (int c = 0; c < 4; ++c) ln_acc(v[r][c], s1, s2);
             s1 = lk_sum(s1);
             s2 = lk_sum(s2);
             if (lk == 0) {
@@ -1520,9 +1554,8 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
                 S1 += lnred[0][q][li];
                 S2 += lnred[1][q][li];
             }
-            const float mean = S1 / (float)H;
-            const float var = fmaxf(S2 / (float)H - mean * mean, 0.f);
-            const float rs = 1.0f / sqrtf(var + 1e-6f);
+            float mean, rs;
+            ln_stats(S1, S2, (float)H, mean, rs);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float4 g4 = *reinterpret_cast<const float4*>(&lnp[1][64 * w + 16 * lk + 4 * r]);
@@ -1530,7 +1563,7 @@ __global__ __launch_bounds__(EF_NW * 64, 1) void stream_fwd_kernel(const StreamA
                 const float ga[4] = {g4.x, g4.y, g4.z, g4.w};
                 const float be[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-                for (int c = 0; c < 4; ++c) v[r][c] = (v[r][c] - mean) * rs * ga[c] + be[c];
+                for (int c = 0; c < 4; ++c) v[r][c] = ln_apply(v[r][c], mean, rs, ga[c], be[c]);
             }
             if (st && w == 0 && lk == 0 && g.MU[l]) {
                 const long long so = (long long)slot * g.st_ss + (long long)y * g.st_sy + m;
@@ -1618,6 +1651,12 @@ void launch_stream_fwd(int head_mode, bool ln, const StreamArgs& a, hipStream_t 
 //     hidden layer, stores its G (and LN statistics) and calls head_write.
 // Counters are zeroed by a memset node before every launch; spins give up after ~2 s and
 // set sync.err (the runtime then reports an error instead of hanging).
+// Residency: a block takes its (cluster, slice) from a launch-wide ticket counter when it
+// starts (sp_ticket), so clusters are formed in the order blocks become resident: at any
+// time a launch has at most one cluster whose blocks are not all resident, and every other
+// cluster can finish and free its CUs.  No launch of a split kernel can therefore wait for
+// blocks that cannot be scheduled, whatever else runs on the device (other streams, other
+// processes), as long as one cluster's F blocks fit on the chip.
 constexpr int SP_NW = 4, SP_NT = SP_NW * 64;
 constexpr long long SP_XB = (long long)EF_H * EF_NC;            // one hidden layer of a tile
 constexpr long long SP_HP = 2 * SP_XB;                          // head partials [8 waves][8 outputs][16]
@@ -1650,6 +1689,15 @@ DEV void sp_wait(const SplitSync& sy, const unsigned* cnt, unsigned target) {
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
+}
+// the block's ticket (cluster * F + slice): one agent-scope atomic on the counter that follows
+// the launch's `clusters` arrival counters
+DEV int sp_ticket(const SplitSync& sy, int clusters, unsigned* bcast) {
+    if (threadIdx.x == 0)
+        *bcast = __hip_atomic_fetch_add((gu32_t*)(sy.cnt + (long long)clusters * SP_CNT_STRIDE), 1u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return (int)*bcast;
 }
 // every wave drains its sc1 stores, then one lane signals; returns the counter value before
 // this block's add (block-uniform via LDS)
@@ -1736,7 +1784,8 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
     __shared__ unsigned bc;
 
     const int tiles = g.M / NC;
-    const int cl = blockIdx.x / F, f = blockIdx.x % F, fb = f * FB;
+    const int ticket = sp_ticket(a.sync, tiles * g.ny * g.nz, &bc);
+    const int cl = ticket / F, f = ticket % F, fb = f * FB;
     const int tl = cl % tiles, yz = cl / tiles;
     const int y = yz % g.ny, z = yz / g.ny;
     const int slot = g.slots[z];
@@ -1768,9 +1817,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
             S1 += lnred[0][w8][col];
             S2 += lnred[1][w8][col];
         }
-        mean = S1 / (float)H;
-        const float var = fmaxf(S2 / (float)H - mean * mean, 0.f);
-        rs = 1.0f / sqrtf(var + 1e-6f);
+        ln_stats(S1, S2, (float)H, mean, rs);
     };
     // normalise the slab in place (thread: features 2 tid, 2 tid + 1) with the statistics in stat[]
     auto ln_slab = [&](int l) {
@@ -1781,7 +1828,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
             const float gv = h ? ga.y : ga.x, bv = h ? be.y : be.x;
             float* row = &slab[(2 * tid + h) * NC];
 #pragma unroll
-            for (int c = 0; c < NC; ++c) row[c] = (row[c] - stat[0][c]) * stat[1][c] * gv + bv;
+            for (int c = 0; c < NC; ++c) row[c] = ln_apply(row[c], stat[0][c], stat[1][c], gv, bv);
         }
     };
     // the block's feature slice of a layer output in the slab -> G (and the LN stats -> MU / RS)
@@ -1859,10 +1906,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
 #pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            s1 += v[h][r][c];
-                            s2 += v[h][r][c] * v[h][r][c];
-                        }
+                        for (int c = 0; c < 4; ++c) ln_acc(v[h][r][c], s1, s2);
                     s1 = lk_sum(s1);
                     s2 = lk_sum(s2);
                     if (lk == 0) {
@@ -1890,7 +1934,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
                         float x = v[h][r][c];
-                        if constexpr (LN) x = (x - mean) * rs * ga[4 * r + c] + be[4 * r + c];
+                        if constexpr (LN) x = ln_apply(x, mean, rs, ga[4 * r + c], be[4 * r + c]);
                         slab[(64 * w + 16 * lk + 4 * r + c) * NC + li] = x;
                     }
             }
@@ -1957,11 +2001,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
                 // LN partials of unsplit wave f TPW + q, in its order (features 64 q + 16 lk + e)
                 float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    const float x = tile[(64 * q + 16 * lk + e) * NC + li];
-                    s1 += x;
-                    s2 += x * x;
-                }
+                for (int e = 0; e < 16; ++e) ln_acc(tile[(64 * q + 16 * lk + e) * NC + li], s1, s2);
                 s1 = lk_sum(s1);
                 s2 = lk_sum(s2);
                 if (lk == 0) {
@@ -2482,11 +2522,11 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
         for (int r = 0; r < 4; ++r) {
             const float wv[4] = {wl[r].x, wl[r].y, wl[r].z, wl[r].w};
 #pragma unroll
-            for (int c = 0; c < 4; ++c) dh[r][c] = 0.f + wv[c] * dv;  // as the general path's sum
+            for (int c = 0; c < 4; ++c) dh[r][c] = mul_rn(wv[c], dv);
         }
         if (gp) {
 #pragma unroll
-            for (int e = 0; e < 16; ++e) gh[e] *= dv;
+            for (int e = 0; e < 16; ++e) gh[e] = mul_rn(gh[e], dv);
             bstore1(rPart, row16_reduce_scatter(gh, li), tid * 4, w5 * 4);
         }
     } else {
@@ -2526,7 +2566,7 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
             for (int j = 0; j < nout; ++j) {
                 float v = 0.f;
 #pragma unroll
-                for (int col = 0; col < NC; ++col) v += gv[col] * dos[j][col];
+                for (int col = 0; col < NC; ++col) v = fmaf(gv[col], dos[j][col], v);
                 part[w5 + tid * nout + j] = v;
             }
         }
@@ -2600,10 +2640,8 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
                     gelu_and_grad_fast(u[r][c], gv, gpr);
                     u[r][c] = gpr;
                     xh[r][c] = (gv - mu) * rs;
-                    scr_l[(4 * r + c) * NC] = dh[r][c] * xh[r][c];
-                    dh[r][c] *= gr[c];  // dh * gamma from here on
-                    s1 += dh[r][c];
-                    s2 += dh[r][c] * xh[r][c];
+                    scr_l[(4 * r + c) * NC] = mul_rn(dh[r][c], xh[r][c]);
+                    dh[r][c] = ln_bwd_acc(dh[r][c], gr[c], xh[r][c], s1, s2);  // dh * gamma from here on
                 }
             }
             s1 = lk_sum(s1);
@@ -2628,7 +2666,7 @@ __global__ __launch_bounds__(EF_NW * 64, LN ? 4 : 1) void stream_bwd_kernel(cons
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) dh[r][c] = rs * (dh[r][c] - c1 - xh[r][c] * c2) * u[r][c];
+                for (int c = 0; c < 4; ++c) dh[r][c] = ln_bwd_du(dh[r][c], xh[r][c], c1, c2, rs, u[r][c]);
         } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -2712,6 +2750,292 @@ void launch_stream_bwd(bool ln, const StreamBwdArgs& a, hipStream_t s) {
     const dim3 grid((a.M / EF_NC) * a.ny * a.nz), block(EF_NW * 64);
     if (ln) hipLaunchKernelGGL((stream_bwd_kernel<true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((stream_bwd_kernel<false>), grid, block, 0, s, a);
+}
+
+// ============================================ split streamed backward (small populations) ==
+// stream_bwd_kernel with each 16-column tile computed by a cluster of F = 2, 4 or 8 blocks
+// (the split streamed forward's scheme): block f owns the 512/F features [fb, fb + 512/F) of
+// every dh_l / du_l; its 4 waves run TPW = 8/F 16x16 tiles of the dX products over the full
+// K (the unsplit k order, W_l^T rows as the A fragments), so every value is the unsplit fp32
+// chain.  The sums over features (LayerNorm backward column statistics) and over columns
+// (bias / LN / head-kernel grad partials) are re-done from LDS images of the block's
+// features in the unsplit order and lane layout ("unsplit wave" w = f TPW + q), so the
+// results are bit-identical to stream_bwd_kernel's.  Hand-offs per layer: the LN column
+// partials (LN only), then du_l (B operand of the next product, staged from the exchange).
+// The critic's dQ/da (columns >= Mg, layer 0) is computed by the cluster's last arriver
+// from the staged du_0, in the unsplit order.
+bool split_bwd_supported(int H, int L, int nout, int M, int Mg) {
+    return H == EF_H && L >= 2 && L <= EF_MAX_LAYERS && nout >= 1 && nout <= 8 && M % EF_NC == 0 &&
+           Mg % EF_NC == 0 && Mg <= M;
+}
+
+template <bool LN, int TPW>
+__global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs g, const SplitSync sync) {
+    constexpr int H = EF_H, NC = EF_NC, NT = SP_NT, F = 8 / TPW, FB = H / F;
+    __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];   // du_l [H][NC] (+ look-ahead slack)
+    __shared__ __attribute__((aligned(16))) float ta[FB * NC];          // the block's dh (raw), then du
+    __shared__ __attribute__((aligned(16))) float tb[FB * NC];          // the block's xhat (LN)
+    __shared__ float cst[2][NC];                                        // c1, c2 per column
+    __shared__ float dos[8][NC];
+    __shared__ unsigned bc;
+
+    const int tiles = g.M / NC;
+    const int ticket = sp_ticket(sync, tiles * g.ny * g.nz, &bc);
+    const int cl = ticket / F, f = ticket % F, fb = f * FB;
+    const int tl = cl % tiles, yz = cl / tiles;
+    const int y = yz % g.ny, z = yz / g.ny;
+    const int slot = g.slots[z];
+    const int c0 = tl * NC;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    const int L = g.L, nout = g.nout;
+    const bool gp = c0 < g.Mg;
+    const float* __restrict__ P = g.params + (long long)slot * g.P + (long long)y * g.ens;
+    const float* __restrict__ PTb = g.paramsT + (long long)slot * g.PT + (long long)y * g.ensT;
+    const rsrc_t rT = make_rsrc(PTb, g.ensT);
+    const long long so = (long long)slot * g.s_ss + (long long)y * g.s_sy + g.coff + c0;
+    const long long sto = (long long)slot * g.st_ss + (long long)y * g.st_sy + g.coff + c0;
+    const long long dso = (long long)slot * g.d_ss + (long long)y * g.d_sy + c0;
+    float* __restrict__ part = gp ? g.part + ((long long)(slot * g.ny + y) * (g.Mg / NC) + tl) * g.NP : nullptr;
+    float* const X = sync.xch + (long long)cl * SP_CLUSTER_STRIDE;
+    const rsrc_t rX = make_rsrc(X, SP_CLUSTER_FLOATS);
+    unsigned* const cnt = sync.cnt + (long long)cl * SP_CNT_STRIDE;
+    unsigned npub = 0;
+    const int w5 = (LN ? 3 : 1) * L * H;
+    // lane layout: tile t, reg r -> feature fb + fl, fl = 16 TPW q + TPW (4 lk + r) + t, column li
+    auto flo = [&](int r, int t) { return 16 * TPW * q + TPW * (4 * lk + r) + t; };
+
+    // ---- head: dh_{L-1} = W_L dout (own features), head-kernel grad partials ----
+    float dh[4][TPW];
+    if (nout == 1) {
+        const float dv = g.dout[(long long)slot * g.dout_ss + (long long)y * g.dout_sy + c0 + li];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) dh[r][t] = mul_rn(P[g.w_off[L] + fb + flo(r, t)], dv);
+        if (gp && q < TPW) {
+            // unsplit wave f TPW + q: G_{L-1}[64 w + 16 lk + e][li] dout, DPP reduce-scatter over the columns
+            const int w8 = f * TPW + q;
+            float gh[16];
+            const float* Gp = g.Ghead + so;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) gh[e] = Gp[(long long)(64 * w8 + 16 * lk + e) * g.ld_s + li];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) gh[e] = mul_rn(gh[e], dv);
+            part[w5 + 64 * w8 + 16 * lk + li] = row16_reduce_scatter(gh, li);
+        }
+    } else {
+        if (tid < 8 * NC) {
+            const int j = tid / NC, col = tid % NC;
+            dos[j][col] = j < nout ? g.dout[(long long)slot * g.dout_ss + (long long)y * g.dout_sy +
+                                            (long long)j * g.ld_o + c0 + col] : 0.f;
+        }
+        __syncthreads();
+        float dj[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dj[j] = dos[j][li];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                const int fe = fb + flo(r, t);
+                float wv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) wv[j] = j < nout ? P[g.w_off[L] + fe * nout + j] : 0.f;
+                float s = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s = fmaf(wv[j], dj[j], s);
+                dh[r][t] = s;
+            }
+        if (gp && tid < FB) {
+            const int fe = fb + tid;
+            float gv[NC];
+            const float* Gr = g.Ghead + so + (long long)fe * g.ld_s;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) gv[c] = Gr[c];
+            for (int j = 0; j < nout; ++j) {
+                float v = 0.f;
+#pragma unroll
+                for (int col = 0; col < NC; ++col) v = fmaf(gv[col], dos[j][col], v);
+                part[w5 + fe * nout + j] = v;
+            }
+        }
+    }
+    // row sum over the 16 columns of an [FB][NC] LDS image, stream_bwd_kernel's order
+    auto row_sum = [&](const float* a, int fl) {
+        const float4* row = reinterpret_cast<const float4*>(&a[fl * NC]);
+        float sv = 0.f;
+#pragma unroll
+        for (int qq = 0; qq < NC / 4; ++qq) {
+            const float4 t4 = row[qq];
+            sv += t4.x + t4.y + t4.z + t4.w;
+        }
+        return sv;
+    };
+
+    float4 ring[SP_PF];
+    const int lo = lk * H + fb + 16 * TPW * q + TPW * li;
+    if (L >= 2) {
+#pragma unroll
+        for (int p = 0; p < SP_PF; ++p) ring[p] = sp_aload<TPW>(rT, (int)g.wt_off[L - 1] + 4 * p * H + lo);
+    }
+    for (int l = L - 1; l >= 0; --l) {
+        // epilogue inputs of layer l (own features)
+        float u[4][TPW];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) u[r][t] = g.U[l][so + (long long)(fb + flo(r, t)) * g.ld_s + li];
+        if constexpr (LN) {
+            const float mu = g.MU[l][sto + li], rs = g.RS[l][sto + li];
+            float xh[4][TPW], gpr[4][TPW];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) {
+                    float gv;
+                    gelu_and_grad_fast(u[r][t], gv, gpr[r][t]);
+                    xh[r][t] = (gv - mu) * rs;
+                    ta[flo(r, t) * NC + li] = dh[r][t];
+                    tb[flo(r, t) * NC + li] = xh[r][t];
+                }
+            __syncthreads();
+            if (q < TPW) {
+                // unsplit wave w8 = f TPW + q: LN bias grads (reduce-scatter of dh), column partials of
+                // dh gamma and dh gamma xhat (16 consecutive features per lane, then the lk sum)
+                const int w8 = f * TPW + q;
+                float v[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) v[e] = ta[(64 * q + 16 * lk + e) * NC + li];
+                if (gp) part[(2 * L + l) * H + 64 * w8 + 16 * lk + li] = row16_reduce_scatter(v, li);
+                float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    (void)ln_bwd_acc(v[e], P[g.g_off[l] + 64 * w8 + 16 * lk + e], tb[(64 * q + 16 * lk + e) * NC + li], s1,
+                                     s2);
+                s1 = lk_sum(s1);
+                s2 = lk_sum(s2);
+                if (lk == 0) {
+                    sp_store1(rX, s1, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + li) * 4));
+                    sp_store1(rX, s2, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + NC + li) * 4));
+                }
+            }
+            if (gp && tid < FB) {
+                // LN scale grads: sum over the columns of dh * xhat (thread = feature)
+                float sv = 0.f;
+                const float4* ra = reinterpret_cast<const float4*>(&ta[tid * NC]);
+                const float4* rb = reinterpret_cast<const float4*>(&tb[tid * NC]);
+#pragma unroll
+                for (int qq = 0; qq < NC / 4; ++qq) {
+                    const float4 a4 = ra[qq], b4 = rb[qq];
+                    sv += mul_rn(a4.x, b4.x) + mul_rn(a4.y, b4.y) + mul_rn(a4.z, b4.z) + mul_rn(a4.w, b4.w);
+                }
+                part[(L + l) * H + fb + tid] = sv;
+            }
+            ++npub;
+            sp_publish(cnt, &bc);
+            sp_wait(sync, cnt, (unsigned)F * npub);
+            if (tid < NC) {
+                float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+                for (int w8 = 0; w8 < EF_NW; ++w8) {
+                    c1 += sp_load1(rX, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + tid) * 4));
+                    c2 += sp_load1(rX, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + NC + tid) * 4));
+                }
+                cst[0][tid] = c1 / (float)H;
+                cst[1][tid] = c2 / (float)H;
+            }
+            __syncthreads();
+            const float c1 = cst[0][li], c2 = cst[1][li];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) {
+                    const float d = mul_rn(dh[r][t], P[g.g_off[l] + fb + flo(r, t)]);  // dh gamma
+                    dh[r][t] = ln_bwd_du(d, xh[r][t], c1, c2, rs, gpr[r][t]);
+                }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) dh[r][t] *= gelu_grad_fast(u[r][t]);
+        }
+        // du_l: DU (dW operand), the LDS image (bias grads), the exchange (next product / dQ/da)
+        const bool need_x = l > 0 || (g.da != nullptr && !gp);
+        __syncthreads();  // ta is free (LN: read above)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                const int fl = flo(r, t);
+                if (gp || g.da == nullptr) g.DU[l][dso + (long long)(fb + fl) * g.ld_d + li] = dh[r][t];
+                ta[fl * NC + li] = dh[r][t];
+                if (need_x) sp_store1(rX, dh[r][t], (int)((((l & 1) * SP_XB) + (long long)(fb + fl) * NC + li) * 4));
+            }
+        __syncthreads();
+        if (gp && tid < FB) part[l * H + fb + tid] = row_sum(ta, tid);  // bias: sum du
+        if (!need_x) break;
+        ++npub;
+        const unsigned before = sp_publish(cnt, &bc);
+        if (l == 0) {
+            // dQ/da of the Q-loss columns by the cluster's last arriver (stream_bwd_kernel's order:
+            // 4 feature quarters of W_0[D0 + j][f] du_0[f][col], then their sum in quarter order)
+            if (before != (unsigned)F * npub - 1) break;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int i = 0; i < (int)(SP_XB / 4 / NT); ++i) {
+                const int e = tid + i * NT;
+                reinterpret_cast<float4*>(slab)[e] = sp_load4(rX, e * 16);  // du_0 (exchange parity 0)
+            }
+            __syncthreads();
+            float* const scr = tb;  // [4 quarters][128] (FB NC >= 1024 floats)
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const int o = tid & 127, qd = (tid >> 7) + 2 * qq, j = o >> 4, col = o & 15;
+                float sacc = 0.f;
+                if (j < g.na) {
+                    const float* wr = P + g.w_off[0] + (long long)(g.D0 + j) * H;
+#pragma unroll 8
+                    for (int fe = qd * (H / 4); fe < (qd + 1) * (H / 4); ++fe) sacc = fmaf(wr[fe], slab[fe * NC + col], sacc);
+                }
+                scr[qd * 128 + o] = sacc;
+            }
+            __syncthreads();
+            if (tid < g.na * NC)
+                g.da[(long long)slot * g.da_ss + (long long)y * g.da_sy + (long long)(tid >> 4) * g.ld_da + (c0 - g.Mg) +
+                     (tid & 15)] = scr[tid] + scr[128 + tid] + scr[256 + tid] + scr[384 + tid];
+            break;
+        }
+        // ---- dh_{l-1} = W_l du_l over the staged du_l (all 512 features) ----
+        sp_wait(sync, cnt, (unsigned)F * npub);
+#pragma unroll
+        for (int i = 0; i < (int)(SP_XB / 4 / NT); ++i) {
+            const int e = tid + i * NT;
+            reinterpret_cast<float4*>(slab)[e] = sp_load4(rX, (int)(((l & 1) * SP_XB) * 4) + e * 16);
+        }
+        __syncthreads();
+        f32x4 acc[TPW];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int wn = (int)g.wt_off[l >= 2 ? l - 1 : l];
+        sp_kloop<TPW>(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lo, lk, li);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) dh[r][t] = acc[t][r];
+    }
+}
+
+void launch_split_bwd(bool ln, int F, const StreamBwdArgs& a, const SplitSync& sy, hipStream_t s) {
+    const dim3 grid((a.M / EF_NC) * a.ny * a.nz * F), block(SP_NT);
+#define FQ_SPB(LNV, T) hipLaunchKernelGGL((split_bwd_kernel<LNV, T>), grid, block, 0, s, a, sy)
+    switch (F) {
+        case 8: if (ln) FQ_SPB(true, 1); else FQ_SPB(false, 1); break;
+        case 4: if (ln) FQ_SPB(true, 2); else FQ_SPB(false, 2); break;
+        default: if (ln) FQ_SPB(true, 4); else FQ_SPB(false, 4); break;
+    }
+#undef FQ_SPB
 }
 
 // Fold the per-tile partials of stream_bwd into the grads (fixed tile order:

@@ -256,7 +256,7 @@ struct fqlpop {
         float* xch = nullptr;
         unsigned* cnt = nullptr;
         long long clusters = 0;    // capacity
-    } split_site[5];
+    } split_site[7];
     unsigned* split_err = nullptr;
     bool split_ok = false;
     bool stream_fwd = false;       // whole-network forward launches (stream_fwd_kernel)
@@ -540,6 +540,49 @@ void gemm(int layout, int epi, const GemmArgs& g, hipStream_t s) {
     launch_gemm_variant(layout, epi, t.tile, t.variant, g, s);
 }
 
+// Split launch sites (fqlpop::split_site): BC forward, Euler flow (sF); one-step, target
+// critic, critic forwards (sM).
+// critic and one-step backwards (sM).  The BC backward (sB) stays unsplit: at most two split
+// launches (one per stream of sF, sM) can then run at once.
+enum { SITE_BCF = 0, SITE_EULER = 1, SITE_OSF = 2, SITE_TGT = 3, SITE_CRF = 4, SITE_CRB = 5, SITE_OSB = 6, SITE_N = 7 };
+constexpr long long kSplitMaxClusters = 128;  // a site with more 16-column tiles runs unsplit
+constexpr long long kSplitMaxBlocks = 256;    // one block per CU (see split_factor)
+
+// Blocks per 16-column tile of a split launch (1 = the unsplit kernel).  Only where the
+// unsplit kernel leaves CUs idle (<= 128 tiles); the most of 8, 4, 2 blocks that keeps the
+// launch within 256 blocks (forced values shrink to fit).  The split kernel runs 2 waves per
+// SIMD and <= 59 KB of LDS per block, so the split launches of the two streams that can run
+// at once (sF, sM) fit the chip together; the blocks take their clusters by ticket, in the
+// order they become resident (kernels.hip, sp_ticket), so a cluster never waits for blocks
+// that cannot be scheduled.  The Euler flow and the LN backward use 4 or 8 blocks (their
+// 2-block forms would spill).
+int split_factor(const fqlpop* h, long long clusters, bool min4) {
+    const int opt = h->opt.split;
+    if (!h->split_ok || opt == 0 || clusters > kSplitMaxClusters) return 1;
+    for (int F = opt >= 2 ? opt : 8; F >= 2; F /= 2) {
+        if (min4 && F < 4) break;
+        if (clusters * F <= kSplitMaxBlocks) return F;
+    }
+    return 1;
+}
+
+// The site's synchronisation state for one launch over `clusters` tiles: its arrival counters
+// and the ticket counter after them are zeroed on `s` first (a memset node in the step's
+// graph).
+SplitSync split_prep(fqlpop* h, int site, long long clusters, hipStream_t s) {
+    fqlpop::SplitSite& st = h->split_site[site];
+    ARGCHK(clusters <= st.clusters, "split launch larger than its site");
+    HIPCHK(hipMemsetAsync(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (clusters + 1), s));
+    return SplitSync{st.xch, st.cnt, h->split_err};
+}
+
+// Blocks per tile of a streamed backward launch (1 = unsplit): the critic (LN: its 2-block
+// form would spill, so 4 or 8) and the one-step actor on sM; never the BC actor on sB.
+int bwd_split(const fqlpop* h, const NetLayout& N, int M, int Mg, int nz) {
+    if (&N == &h->bc || !split_bwd_supported(N.H, N.L, N.out_dim, M, Mg)) return 1;
+    return split_factor(h, (long long)(M / 16) * N.E * nz, N.ln);
+}
+
 // Forward of the hidden stack of `N` over `M` columns of input X (ld = ldx).
 // U[l]/G[l]: pre-activation and layer output buffers (ld = ldx).  store_u:
 // keep u (needed by backward / LN); otherwise G[l] = gelu(u) directly.
@@ -725,7 +768,15 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         ARGCHK((long long)(M / 16) * N.E * c.nz <= h->phase_blocks, "phase probe: too many blocks");
         a.phase = h->phase_dev;
     }
-    if (!(skip_mask() & (&N == &h->critic ? 32 : &N == &h->bc ? 64 : 128))) launch_stream_bwd(N.ln, a, s);
+    if (!(skip_mask() & (&N == &h->critic ? 32 : &N == &h->bc ? 64 : 128))) {
+        const int F = bwd_split(h, N, M, Mg, c.nz);
+        if (F > 1) {
+            const long long clusters = (long long)(M / 16) * N.E * c.nz;
+            launch_split_bwd(N.ln, F, a, split_prep(h, &N == &h->critic ? SITE_CRB : SITE_OSB, clusters, s), s);
+        } else {
+            launch_stream_bwd(N.ln, a, s);
+        }
+    }
     hipEvent_t ev = nullptr;
     if (sw != s) {
         ev = next_event(h);
@@ -862,38 +913,6 @@ AdamArgs adam_args(const Ctx& c, int ni) {
 void adam_net(const Ctx& c, hipStream_t s, int ni) {
     const AdamArgs a = adam_args(c, ni);
     if (a.n_chunks > 0) launch_adam(a, s);
-}
-
-// Split launch sites (fqlpop::split_site): BC forward, Euler flow (sF); one-step, target
-// critic, critic forwards (sM).
-enum { SITE_BCF = 0, SITE_EULER = 1, SITE_OSF = 2, SITE_TGT = 3, SITE_CRF = 4, SITE_N = 5 };
-constexpr long long kSplitMaxClusters = 128;  // a site with more 16-column tiles runs unsplit
-constexpr long long kSplitMaxBlocks = 256;    // one block per CU (see split_factor)
-
-// Blocks per 16-column tile of a split launch (1 = the unsplit kernel).  Only where the
-// unsplit kernel leaves CUs idle (<= 128 tiles); the most of 8, 4, 2 blocks that keeps the
-// launch within 256 blocks (forced values shrink to fit).  The split kernel runs 2 waves per
-// SIMD and <= 59 KB of LDS per block, so the split launches of the two streams that can run
-// at once (sF, sM) fit the chip together and every cluster's blocks are resident at the same
-// time (their hand-off waits need that).  The Euler flow uses 4 or 8 (its 2-block form
-// would spill).
-int split_factor(const fqlpop* h, long long clusters, bool euler) {
-    const int opt = h->opt.split;
-    if (!h->split_ok || opt == 0 || clusters > kSplitMaxClusters) return 1;
-    for (int F = opt >= 2 ? opt : 8; F >= 2; F /= 2) {
-        if (euler && F < 4) break;
-        if (clusters * F <= kSplitMaxBlocks) return F;
-    }
-    return 1;
-}
-
-// The site's synchronisation state for one launch over `clusters` tiles: its counters are
-// zeroed on `s` first (a memset node in the step's graph).
-SplitSync split_prep(fqlpop* h, int site, long long clusters, hipStream_t s) {
-    fqlpop::SplitSite& st = h->split_site[site];
-    ARGCHK(clusters <= st.clusters, "split launch larger than its site");
-    HIPCHK(hipMemsetAsync(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * clusters, s));
-    return SplitSync{st.xch, st.cnt, h->split_err};
 }
 
 // One whole-network forward launch (stream_fwd_kernel).  `arena` + N.off is the
@@ -1725,13 +1744,13 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         h->split_ok = h->stream_fwd && eo.split != 0;
         if (h->split_ok) {
             const long long tiles_per_member[SITE_N] = {B2 / 16, B / 16, B3 / 16, (long long)E * B / 16,
-                                                        (long long)E * B2 / 16};
+                                                        (long long)E * B2 / 16, (long long)E * B2 / 16, B / 16};
             for (int si = 0; si < SITE_N; ++si) {
                 auto& st = h->split_site[si];
                 st.clusters = std::min(kSplitMaxClusters, tiles_per_member[si] * n);
                 HIPCHK(hipMalloc(&st.xch, sizeof(float) * split_cluster_floats() * st.clusters));
-                HIPCHK(hipMalloc(&st.cnt, sizeof(unsigned) * split_counter_stride() * st.clusters));
-                HIPCHK(hipMemset(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * st.clusters));
+                HIPCHK(hipMalloc(&st.cnt, sizeof(unsigned) * split_counter_stride() * (st.clusters + 1)));
+                HIPCHK(hipMemset(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (st.clusters + 1)));
             }
             HIPCHK(hipMalloc(&h->split_err, 64));
             HIPCHK(hipMemset(h->split_err, 0, 64));
