@@ -556,12 +556,12 @@ constexpr long long kSplitMaxBlocks = 256;    // one block per CU (see split_fac
 // order they become resident (kernels.hip, sp_ticket), so a cluster never waits for blocks
 // that cannot be scheduled.  The Euler flow and the LN backward use 4 or 8 blocks (their
 // 2-block forms would spill).
-int split_factor(const fqlpop* h, long long clusters, bool min4) {
+int split_factor(const fqlpop* h, long long clusters, bool min4, long long max_blocks = kSplitMaxBlocks) {
     const int opt = h->opt.split;
     if (!h->split_ok || opt == 0 || clusters > kSplitMaxClusters) return 1;
     for (int F = opt >= 2 ? opt : 8; F >= 2; F /= 2) {
         if (min4 && F < 4) break;
-        if (clusters * F <= kSplitMaxBlocks) return F;
+        if (clusters * F <= max_blocks) return F;
     }
     return 1;
 }
@@ -577,10 +577,11 @@ SplitSync split_prep(fqlpop* h, int site, long long clusters, hipStream_t s) {
 }
 
 // Blocks per tile of a streamed backward launch (1 = unsplit): the critic (LN: its 2-block
-// form would spill, so 4 or 8) and the one-step actor on sM; never the BC actor on sB.
+// form would spill, so 4 or 8, up to 2 blocks per CU: 4 x 128 tiles for a 2-member
+// population) and the one-step actor on sM; never the BC actor on sB.
 int bwd_split(const fqlpop* h, const NetLayout& N, int M, int Mg, int nz) {
     if (&N == &h->bc || !split_bwd_supported(N.H, N.L, N.out_dim, M, Mg)) return 1;
-    return split_factor(h, (long long)(M / 16) * N.E * nz, N.ln);
+    return split_factor(h, (long long)(M / 16) * N.E * nz, N.ln, N.ln ? 2 * kSplitMaxBlocks : kSplitMaxBlocks);
 }
 
 // Forward of the hidden stack of `N` over `M` columns of input X (ld = ldx).
@@ -1549,6 +1550,8 @@ int fqlpop_set_engine_option(const char* name, int value) {
         for (const EngineOptionRef& o : kEngineOptions)
             if (std::strcmp(o.name, name) == 0) {
                 ARGCHK(value >= o.lo && value <= o.hi, std::string("engine option ") + name + " out of range");
+                ARGCHK(o.field != &EngineOptions::split || value <= 2 || value == 4 || value == 8,
+                       "engine option split: 0, 1, 2, 4 or 8");
                 g_engine_opts.*o.field = value;
                 return;
             }

@@ -4,9 +4,15 @@ FETCH_SIZE (KiB) reports half the bytes of wide coalesced streaming reads, so
 it is doubled; WRITE_SIZE (KiB) is taken as is.
 
   python pmc_summary.py <fetch counter_collection.csv> <write counter_collection.csv> <kernel substring> [out.json]
+
+The JSON records the source commit (FQ_COMMIT in the environment: the box has no .git, so
+the caller passes it) and the UTC date of the summary; bench.py copies both into the
+roofline's traffic_source.
 """
 import csv
+import datetime
 import json
+import os
 import sys
 
 
@@ -29,7 +35,10 @@ print(f"traffic (corrected) {(2 * f + w) / 1e6:.3f} MB/launch")
 
 if len(sys.argv) > 4:
     with open(sys.argv[4], "w") as fo:
-        json.dump({"kernel_regex": sys.argv[3], "members": 16, "dispatches": len(fetch),
+        json.dump({"kernel_regex": sys.argv[3], "members": int(os.environ.get("FQ_MEMBERS", "16")),
+                   "workload": os.environ.get("FQ_WORKLOAD", "cube"), "dispatches": len(fetch),
+                   "commit": os.environ.get("FQ_COMMIT"),
+                   "date": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
                    "fetch_size_bytes_raw": f, "fetch_bytes_corrected_x2": 2 * f, "write_bytes": w,
                    "traffic_bytes_per_launch": 2 * f + w,
                    "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 counts 64 B per 128 B request); "

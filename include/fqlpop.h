@@ -77,17 +77,16 @@ const char* fqlpop_last_error(void);
  * select alternate code paths and stream schedules with the same results
  * (bit-identical, or the per-layer / unfused paths within the parity tolerance),
  * for tests and profiling; there is no reference counterpart.  Names:
- *   euler_fused, stream_fwd, stream_bwd, fused_adam, cdw_sb, serial  (0/1)
- *   streams (3/4), prio (0..2), dw_tile_critic / dw_tile_actor (0..10), adam_nt (0..3),
- *   dw_stagger (0..256: start offsets of the fused dW + optimiser launch's first blocks),
- *   xstep (0/1: inside one fqlpop_step call, each step's critic dW / optimiser runs at the
- *   head of the next step's graph, beside its sampling and actor forwards),
- *   bc_late (0..2: the BC update after the critic forward / backward of the main chain),
- *   fuse_dq (0/1: the critic-loss gradient seeds written by the critic forward's head),
- *   early_join (0..2: the main chain's waits for the flow / BC loss moved ahead).
+ *   euler_fused, stream_fwd, stream_bwd, fused_adam, serial  (0/1)
+ *   dw_tile_critic / dw_tile_actor (0..10), adam_nt (0..3),
+ *   split (0 off, 1 auto, 2 / 4 / 8: small populations run the streamed forwards, the
+ *   Euler flow and the critic / one-step backwards as clusters of 2-8 blocks per 16-column
+ *   tile; bit-identical to the unsplit kernels).
  * The defaults are the measured-fastest configuration.  Unknown names or values
- * out of range: FQLPOP_E_ARG.  The production library reads no environment
- * variable; result-changing timing switches exist only in diagnostic builds. */
+ * out of range: FQLPOP_E_ARG.  (Round 3's schedule experiments that measured slower --
+ * streams, prio, cdw_sb, dw_stagger, xstep, bc_late, fuse_dq, early_join -- were
+ * removed.)  The production library reads no environment variable; result-changing
+ * timing switches exist only in diagnostic builds. */
 int fqlpop_set_engine_option(const char* name, int value);
 int fqlpop_get_engine_option(const char* name, int* value);
 int fqlpop_reset_engine_options(void);

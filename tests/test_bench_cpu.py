@@ -62,3 +62,18 @@ def test_removed_schedule_experiments_are_unknown_options():
         with pytest.raises(fqlpop.FqlpopError):
             fqlpop.set_engine_option(name, 1)
     fqlpop.reset_engine_options()
+
+
+def test_split_option_values():
+    """Engine option split: 0 (off), 1 (auto, the default), or 2 / 4 / 8 blocks per tile."""
+    import pytest
+    import fqlpop
+    fqlpop.reset_engine_options()
+    assert fqlpop.get_engine_option("split") == 1
+    for v in (0, 2, 4, 8):
+        fqlpop.set_engine_option("split", v)
+        assert fqlpop.get_engine_option("split") == v
+    for v in (3, 5, 6, 7, 9, -1):
+        with pytest.raises(fqlpop.FqlpopError):
+            fqlpop.set_engine_option("split", v)
+    fqlpop.reset_engine_options()

@@ -26,7 +26,9 @@ def test_bench_json_contract():
     assert d["steps"] == 4 and d["warmup"] == 2 and d["n_gpus"] == 1
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         assert d["metric"] == json.load(f)["metric"]  # the north-star metric, verbatim
-    assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
+    # the default workload: the 16-member population sharded over the ranks (strong scaling)
+    assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "strong"
+    assert d["config"]["population"] == 16 and d["config"]["members_this_rank"] == 16
     assert d["config"]["info_finite"] is True
     assert abs(d["value"] - 16 * 1000.0 / d["ms_per_step"]) <= 1e-3 * d["value"] + 1.0
     rf = d["roofline"]
@@ -57,7 +59,7 @@ def test_bench_self_launches_ranks_sharing_the_device():
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]  # stdout: the JSON line only
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["share_device"] is True
+    assert d["n_gpus"] == 2 and d["config"]["share_device"] is True and d["scaling"] == "weak"
     assert d["config"]["global_batch"] == 256 * 4 * 2
     assert abs(d["value"] - 8 * 1000.0 / d["ms_per_step"]) <= 1e-3 * d["value"] + 1.0
     assert d["config"]["info_finite"] is True
@@ -74,3 +76,37 @@ def test_production_library_ignores_timing_switches():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=ROOT, env=e)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "smoke ok" in r.stdout
+
+
+def test_bench_population_is_sharded_over_ranks():
+    """--population P (the default, P = 16): the P members are dealt round-robin to the
+    ranks (strong scaling), the metric names the whole population, value counts P members."""
+    r = _bench(["--gpus", "2", "--share-device", "--population", "6", "--steps", "4", "--warmup", "2", "--rows",
+                "20000", "--no-cpu-baseline", "--eval-envs", "0", "--envmodel-train-steps", "0", "--kernel-iters",
+                "2", "--preheat-ms", "20"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    assert d["scaling"] == "strong" and d["config"]["population"] == 6
+    assert d["config"]["members_this_rank"] == 3 and d["config"]["members_per_gpu"] == 3
+    assert "over 6-" in d["metric"]
+    assert abs(d["value"] - 6 * 1000.0 / d["ms_per_step"]) <= 1e-3 * d["value"] + 1.0
+
+
+def test_two_hardware_queues_smoke_and_bench():
+    """GPU_MAX_HW_QUEUES=2 (a legal HIP runtime setting; the box defaults to 4) from the
+    start of a fresh process: smoke() and a 16-member bench run complete.  Round 3 saw a
+    crash inside the HIP runtime during the first graph captures under this setting."""
+    code = ("import sys; sys.path[:0] = [%r, %r]; import __graft_entry__ as g; g.smoke()"
+            % (ROOT, os.path.join(ROOT, "flow-q-learning_amd")))
+    e = dict(os.environ, GPU_MAX_HW_QUEUES="2")
+    for k in [k for k in e if k.startswith("FQLPOP_")]:
+        del e[k]
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=ROOT, env=e)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "smoke ok" in r.stdout
+    r = _bench(["--steps", "4", "--warmup", "2", "--rows", "20000", "--no-cpu-baseline", "--eval-envs", "0",
+                "--envmodel-train-steps", "0", "--kernel-iters", "2", "--preheat-ms", "20"],
+               env={"GPU_MAX_HW_QUEUES": "2"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    assert d["config"]["info_finite"] is True and d["value"] > 0

@@ -53,6 +53,24 @@ def _run(rank, world, port, save_dir, strategy_kind, plain=False):
                 self.population = set(D.ordered(self.population)[0::2][:3])
             return self.population
 
+    class DropAndRevive(HpoStrategy):
+        """After the first evaluation keep the candidates at even positions of the ordered
+        list (on 2 ranks: rank 1 retires all of its members, rank 0 gives one survivor to
+        rank 1), after the second bring every candidate back: a retired member resumes on
+        the rank that holds its state, or is sent to the rank place_new picks."""
+        def __init__(self, population):
+            super().__init__(population, 0)
+            self.all = set(population)
+            self.n_eval = {}
+
+        def update(self, candidate, performance):
+            self.n_eval[candidate] = self.n_eval.get(candidate, 0) + 1
+
+        def sample(self):
+            rounds = max(self.n_eval.values()) if self.n_eval else 0
+            self.population = set(D.ordered(self.all)[0::2]) if rounds == 1 else set(self.all)
+            return self.population
+
     task = OfflineTaskWithSimulatedEvaluations(n_rows=20_000, n_val_rows=2_000, num_evaluation_envs=16,
                                                max_episode_steps=25)
     agent = AgentConfig(actor_hidden_dims=(H,) * 4, value_hidden_dims=(H,) * 4, batch_size=64)
@@ -61,6 +79,8 @@ def _run(rank, world, port, save_dir, strategy_kind, plain=False):
                                                                (300.0, 5), (1000.0, 6)]}
     if strategy_kind == "halving":
         strategy = SuccessiveHalving(configs, total_evaluations=12, fraction=0.5, history_length=1)
+    elif strategy_kind == "revive":
+        strategy = DropAndRevive(configs)
     else:
         strategy = KeepEven(configs)
     tr = Trainer(task, strategy, cfg) if plain else DistributedTrainer(task, strategy, cfg)
@@ -105,7 +125,7 @@ def _two_ranks(tmp_path, kind):
     return sorted(outs, key=lambda o: o["rank"])
 
 
-@pytest.mark.parametrize("kind", ["halving", "keep_even"])
+@pytest.mark.parametrize("kind", ["halving", "keep_even", "revive"])
 def test_two_ranks_match_one_rank(tmp_path, kind):
     """The baseline is the plain single-process Trainer (what tune_alpha runs at
     WORLD_SIZE=1); DistributedTrainer at one rank must agree with it too."""
@@ -117,8 +137,8 @@ def test_two_ranks_match_one_rank(tmp_path, kind):
     r0, r1 = _two_ranks(tmp_path, kind)
     # the same decisions and scores on every rank, equal to the one-rank run
     assert r0["candidates"] == r1["candidates"] == one["candidates"]
-    # halving: 6 -> 3 at the 3-evaluation milestone; keep_even: 6 -> 3 -> 2
-    assert len(one["candidates"]) == (3 if kind == "halving" else 2)
+    # halving: 6 -> 3 at the 3-evaluation milestone; keep_even: 6 -> 3 -> 2; revive: 6 -> 3 -> 6
+    assert len(one["candidates"]) == {"halving": 3, "keep_even": 2, "revive": 6}[kind]
     assert r0["scores"] == r1["scores"] == one["scores"]
     # the survivors are split over the ranks (evened out after pruning) ...
     assert set(r0["params"]).isdisjoint(r1["params"])
