@@ -193,9 +193,11 @@ void launch_stream_fwd(int head_mode, bool ln, const StreamArgs& a, hipStream_t 
 // L2 / MALL (kernels.hip, "split streamed forward"): bit-identical to the unsplit
 // kernels, and F times as many blocks, so that 1-4 members fill the chip.
 struct SplitSync {
-    float* xch;             // exchange, split_cluster_floats() per cluster
-    unsigned* cnt;          // arrival counters, split_counter_stride() apart, zeroed before every launch
-    unsigned* err;          // set to nonzero when a hand-off wait gives up (results then invalid)
+    unsigned long long* xch;  // exchange words {value, tag}, split_cluster_bytes() per cluster
+    unsigned* cnt;            // counters split_counter_stride() apart: [clusters] last-arriver, then the
+                              // ticket and the exit counter; zeroed before every launch
+    unsigned* gen;            // the site's launch generation (never zeroed; the tags' high bits)
+    unsigned* err;            // set to nonzero when a hand-off wait gives up (results then invalid)
 };
 struct SplitFwdArgs {
     StreamArgs s;           // as launch_stream_fwd (Euler: params, w_off, b_off, x0 = state after step
@@ -206,7 +208,7 @@ struct SplitFwdArgs {
     unsigned long long* probe;   // optional per-block {start, end} stamps
     SplitSync sync;
 };
-long long split_cluster_floats();
+long long split_cluster_bytes();
 int split_counter_stride();
 bool split_fwd_supported(int H, int L, int K0, int nout, int M);
 // F = 8, 4 or 2 blocks per 16-column tile; grid = tiles x ny x nz x F blocks of 256 threads

@@ -1637,86 +1637,127 @@ void launch_stream_fwd(int head_mode, bool ln, const StreamArgs& a, hipStream_t 
 //     the unsplit lane layout (two "unsplit waves" per wave), into the LDS slab: no hand-off;
 //   * hidden layer l >= 1: A fragments W_l[4s + lk][feature] (TPW consecutive features per
 //     lane: dword / dwordx2 / dwordx4 loads, an 8-deep ring that runs across layers), B from
-//     the LDS slab; the epilogue publishes GELU(u) of the block's features to the cluster's
-//     exchange (write-through sc1 stores), and LayerNorm's column partials of the block's
-//     "unsplit waves", summed in the unsplit order from an LDS image of the block's tile;
-//   * hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, valid form 1): every storing
-//     wave drains (s_waitcnt vmcnt(0)), a barrier, ONE lane adds to the cluster's counter
-//     (agent-scope atomic); a consumer polls it (relaxed sc1 load + s_sleep, bounded), then
-//     stages the exchange into its LDS slab with sc1 loads (no plain load of handed-off bytes)
-//     and normalises it (LN: the 8 unsplit-wave partials summed in the unsplit order);
+//     the LDS slab in FRAGMENT ORDER (sp_fidx: one ds_read_b128 gives a lane the B values of
+//     4 k-steps); the epilogue publishes GELU(u) of the block's features, and LayerNorm's
+//     column partials of the block's "unsplit waves" (summed in the unsplit order from an LDS
+//     image of the block's tile);
+//   * hand-off by tagged granules (MI355X_MICROARCH.md price list, handoff-1to1 / allgather;
+//     cdna_hip_programming.md Guideline 16, R2): every published value is one 8-byte
+//     {value, tag} word written by one agent-scope atomic store; a consumer re-reads the
+//     words of a layer (16-byte sc1 loads) until every tag is the hand-off's, and writes the
+//     values into its LDS slab.  The data is its own flag: no drain, no counter, no poll of a
+//     separate word.  tag = launch generation << 8 | hand-off index + 1; the generation is a
+//     per-site word the last exiting block of every launch increments, so words left by an
+//     earlier launch never match;
 //   * head: the Euler flow publishes every block's unsplit-wave head partials and every block
 //     sums the 8 in the unsplit order (x += v / S for the next step); the forward's head is
-//     computed by the cluster's LAST arriver (told by its counter add), which stages the last
-//     hidden layer, stores its G (and LN statistics) and calls head_write.
-// Counters are zeroed by a memset node before every launch; spins give up after ~2 s and
-// set sync.err (the runtime then reports an error instead of hanging).
+//     computed by the cluster's LAST arriver (told by its add to the cluster's counter), which
+//     stages the last hidden layer, stores its G (and LN statistics) and calls head_write.
+// The counters (cluster, ticket, exit) are zeroed by a memset node before every launch; spins
+// give up after ~2 s and set sync.err (the runtime then reports an error instead of hanging).
 // Residency: a block takes its (cluster, slice) from a launch-wide ticket counter when it
-// starts (sp_ticket), so clusters are formed in the order blocks become resident: at any
-// time a launch has at most one cluster whose blocks are not all resident, and every other
-// cluster can finish and free its CUs.  No launch of a split kernel can therefore wait for
-// blocks that cannot be scheduled, whatever else runs on the device (other streams, other
-// processes), as long as one cluster's F blocks fit on the chip.
+// starts (sp_begin), so clusters are formed in the order blocks become resident: at any time
+// a launch has at most one cluster whose blocks are not all resident, and every other cluster
+// can finish and free its CUs.  No split launch can therefore wait for blocks that cannot be
+// scheduled, whatever else runs on the device (other streams, other processes), as long as
+// one cluster's F blocks fit on the chip.
 constexpr int SP_NW = 4, SP_NT = SP_NW * 64;
-constexpr long long SP_XB = (long long)EF_H * EF_NC;            // one hidden layer of a tile
-constexpr long long SP_HP = 2 * SP_XB;                          // head partials [8 waves][8 outputs][16]
-constexpr long long SP_LP = SP_HP + 8 * 8 * EF_NC;              // LN partials [2 parities][8 waves][2][16]
-constexpr long long SP_CLUSTER_FLOATS = SP_LP + 2 * 8 * 2 * EF_NC;
-constexpr int SP_CNT_STRIDE = 16;                               // counters 64 B apart
+constexpr int SP_XG = EF_H * EF_NC;                              // granules of one hidden layer of a tile
+constexpr int SP_G_HP = 2 * SP_XG;                               // head partials [8 waves][8 outputs][16]
+constexpr int SP_G_LP = SP_G_HP + 8 * 8 * EF_NC;                 // LN partials [2 parities][8 waves][2][16]
+constexpr int SP_G_N = SP_G_LP + 2 * 8 * 2 * EF_NC;
+constexpr long long SP_CLUSTER_GRANULES = (SP_G_N + 31) / 32 * 32;
+constexpr int SP_CNT_STRIDE = 16;                                // counters 64 B apart
 constexpr unsigned SP_SPIN_LIMIT = 1u << 21;
 
-constexpr long long SP_CLUSTER_STRIDE = (SP_CLUSTER_FLOATS + 63) / 64 * 64;
-long long split_cluster_floats() { return SP_CLUSTER_STRIDE; }
+long long split_cluster_bytes() { return SP_CLUSTER_GRANULES * 8; }
 int split_counter_stride() { return SP_CNT_STRIDE; }
 
 typedef __attribute__((address_space(1))) unsigned int gu32_t;
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 
-DEV unsigned sp_poll(const unsigned* cnt) {
-    return __hip_atomic_load((const gu32_t*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// element index of (feature k, column col) in the fragment-order slab / exchange: k-step
+// s = k >> 2 of lane (lk = k & 3, col) is component s & 3 of float4 (s >> 2) * 64 + lane
+DEV int sp_fidx(int k, int col) { return ((((k >> 4) << 6) + ((k & 3) << 4) + col) << 2) + ((k >> 2) & 3); }
+
+DEV void sp_fail(const SplitSync& sy) {
+    __hip_atomic_store((gu32_t*)sy.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// lane 0 of the block waits until the cluster's counter reaches `target`; the barrier after it
-// releases the other waves (their loads of the exchange are all sc1)
-DEV void sp_wait(const SplitSync& sy, const unsigned* cnt, unsigned target) {
+// block start: the ticket (cluster * F + slice) and the launch generation, block-uniform
+DEV int sp_begin(const SplitSync& sy, int clusters, unsigned* bc) {
     if (threadIdx.x == 0) {
-        unsigned spins = 0;
-        while (sp_poll(cnt) < target) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > SP_SPIN_LIMIT) {
-                __hip_atomic_store((gu32_t*)sy.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
+        bc[0] = __hip_atomic_fetch_add((gu32_t*)(sy.cnt + (long long)clusters * SP_CNT_STRIDE), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        bc[1] = __hip_atomic_load((const gu32_t*)sy.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
+    return (int)bc[0];
 }
-// the block's ticket (cluster * F + slice): one agent-scope atomic on the counter that follows
-// the launch's `clusters` arrival counters
-DEV int sp_ticket(const SplitSync& sy, int clusters, unsigned* bcast) {
+// block end (every block, every path): the last one to exit advances the site's generation
+DEV void sp_end(const SplitSync& sy, int clusters, int blocks) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned e = __hip_atomic_fetch_add((gu32_t*)(sy.cnt + (long long)(clusters + 1) * SP_CNT_STRIDE), 1u,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == (unsigned)blocks - 1) __hip_atomic_fetch_add((gu32_t*)sy.gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+DEV unsigned sp_tag(unsigned gen, unsigned phase) { return (gen << 8) | ((phase + 1) & 255u); }
+// publish one value (an 8-byte {value, tag} word, one atomic store)
+DEV void gx_put(unsigned long long* X, int gi, float v, unsigned tag) {
+    __hip_atomic_store((gu64_t*)(X + gi), ((unsigned long long)tag << 32) | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+// read one published value, waiting for its tag
+DEV float gx_get(const unsigned long long* X, int gi, unsigned tag, const SplitSync& sy) {
+    unsigned spins = 0;
+    while (true) {
+        const unsigned long long x = __hip_atomic_load((const gu64_t*)(X + gi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(x >> 32) == tag) return __builtin_bit_cast(float, (unsigned)x);
+        if (++spins > SP_SPIN_LIMIT) {
+            sp_fail(sy);
+            return 0.f;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+// stage one published layer (SP_XG words from granule g0) into the fragment-order slab: each
+// thread re-reads its 16-byte chunks (two words, sc1 loads) until both tags match
+DEV void gx_stage(rsrc_t rX, int g0, unsigned tag, float* slab, const SplitSync& sy) {
+    constexpr int CH = 8, PASSES = SP_XG / 2 / SP_NT / CH;  // 2 passes of 8 chunks per thread (32 VGPRs)
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+        unsigned pending = (1u << CH) - 1u, spins = 0;
+        uint4 v[CH];
+        while (true) {
+#pragma unroll
+            for (int i = 0; i < CH; ++i)
+                if (pending & (1u << i))
+                    v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         rX, (g0 + 2 * ((int)threadIdx.x + (ps * CH + i) * SP_NT)) * 8, 0, 16));
+#pragma unroll
+            for (int i = 0; i < CH; ++i)
+                if ((pending & (1u << i)) && v[i].y == tag && v[i].w == tag) {
+                    *reinterpret_cast<float2*>(&slab[2 * ((int)threadIdx.x + (ps * CH + i) * SP_NT)]) =
+                        float2{__builtin_bit_cast(float, v[i].x), __builtin_bit_cast(float, v[i].z)};
+                    pending &= ~(1u << i);
+                }
+            if (pending == 0) break;
+            if (++spins > SP_SPIN_LIMIT) {
+                sp_fail(sy);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+// the cluster's last arriver (after its words are written): one add to the cluster's counter
+DEV bool sp_last(const SplitSync& sy, int cl, int F, unsigned* bc) {
     if (threadIdx.x == 0)
-        *bcast = __hip_atomic_fetch_add((gu32_t*)(sy.cnt + (long long)clusters * SP_CNT_STRIDE), 1u, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
+        bc[0] = __hip_atomic_fetch_add((gu32_t*)(sy.cnt + (long long)cl * SP_CNT_STRIDE), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    return (int)*bcast;
-}
-// every wave drains its sc1 stores, then one lane signals; returns the counter value before
-// this block's add (block-uniform via LDS)
-DEV unsigned sp_publish(unsigned* cnt, unsigned* bcast) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        *bcast = __hip_atomic_fetch_add((gu32_t*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    return *bcast;
-}
-DEV void sp_store1(rsrc_t r, float v, int off_b) {  // write-through (sc1) dword store
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, off_b, 0, 16);
-}
-DEV float4 sp_load4(rsrc_t r, int off_b) {  // sc1 (L1-bypassing) dwordx4 load
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off_b, 0, 16));
-}
-DEV float sp_load1(rsrc_t r, int off_b) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off_b, 0, 16));
+    return bc[0] == (unsigned)F - 1;
 }
 
 // A fragments of TPW consecutive features: W[k][col .. col + TPW - 1] (components 0..TPW-1)
@@ -1733,23 +1774,28 @@ DEV float4 sp_aload(rsrc_t r, int elem_off) {
     }
 }
 
-// One split hidden layer's k-loop (see ef_kloop): acc[t] += W[k][col + t] xs[k][li] over the
-// NS k-steps; ring[] holds this layer's first SP_PF k-steps on entry and the next layer's
-// (w_next) on exit.  lo = lk * H + col.
+// One split hidden layer's k-loop (see ef_kloop): acc[t] += W[k][col + t] x[k][li] over the
+// NS k-steps, B from the fragment-order slab (one float4 = 4 k-steps, read a group ahead);
+// ring[] holds this layer's first SP_PF k-steps on entry and the next layer's (w_next) on
+// exit.  lo = lk * H + col.
 constexpr int SP_PF = 8;
 template <int TPW>
 DEV void sp_kloop(f32x4 (&acc)[TPW], float4 (&ring)[SP_PF], rsrc_t rW, const float* xs, int NS, int w_cur,
-                  int w_next, int lo, int lk, int li) {
-    constexpr int H = EF_H, NC = EF_NC, PF = SP_PF;
-    float bnext = xs[lk * NC + li];
+                  int w_next, int lo, int lane) {
+    constexpr int H = EF_H, PF = SP_PF;
+    const float4* x4 = reinterpret_cast<const float4*>(xs);
+    float4 bn = x4[lane], b4 = bn;
     int s0 = 0;
     do {
         const int rbase = (s0 + PF < NS ? w_cur + 4 * (s0 + PF) * H : w_next) + lo;
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
             const int s = s0 + p;
-            const float b = bnext;
-            bnext = xs[(4 * (s + 1) + lk) * NC + li];
+            if ((p & 3) == 0) {
+                b4 = bn;
+                bn = x4[((s >> 2) + 1) * 64 + lane];  // the next group (past the end: slack)
+            }
+            const float b = (p & 3) == 0 ? b4.x : (p & 3) == 1 ? b4.y : (p & 3) == 2 ? b4.z : b4.w;
             __builtin_amdgcn_sched_barrier(0);
             const float4 a = ring[p];
             acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b, acc[0], 0, 0, 0);
@@ -1767,7 +1813,7 @@ DEV void sp_kloop(f32x4 (&acc)[TPW], float4 (&ring)[SP_PF], rsrc_t rW, const flo
 }
 
 bool split_fwd_supported(int H, int L, int K0, int nout, int M) {
-    // L >= 3: a hand-off wait lies between two steps' head-partial writes (Euler)
+    // L >= 3: a hand-off lies between two steps' head-partial writes (Euler)
     return H == EF_H && L >= 3 && L <= EF_MAX_LAYERS && K0 <= EF_K0MAX && nout <= 8 && M % EF_NC == 0;
 }
 
@@ -1775,16 +1821,18 @@ template <int MODE, bool LN, bool EULER, int TPW>
 __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs a) {
     constexpr int H = EF_H, NC = EF_NC, NT = SP_NT, PF = EF_PF, F = 8 / TPW, FB = H / F;
     const StreamArgs& g = a.s;
-    __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];         // layer input [H][NC] (+ look-ahead slack)
-    __shared__ __attribute__((aligned(16))) float in0[EF_K0MAX * NC + 64];   // layer-0 input
-    __shared__ __attribute__((aligned(16))) float tile[FB * NC];             // the block's layer output (LN / head)
+    __shared__ __attribute__((aligned(16))) float slab[H * NC + 256];        // layer input, fragment order (+ slack)
+    __shared__ __attribute__((aligned(16))) float in0[EF_K0MAX * NC + 64];   // layer-0 input [K0][NC]
+    __shared__ __attribute__((aligned(16))) float tile[FB * NC];             // the block's layer output [FB][NC]
     __shared__ float lnred[2][8][NC];                                        // unsplit-wave LN partials
     __shared__ float stat[2][NC];                                            // column mean / rstd
+    __shared__ float lng[2][H];                                              // LN scale / bias of a staged layer
     __shared__ float hred[8][8][NC];                                         // unsplit-wave head partials
-    __shared__ unsigned bc;
+    __shared__ unsigned bc[2];
 
-    const int tiles = g.M / NC;
-    const int ticket = sp_ticket(a.sync, tiles * g.ny * g.nz, &bc);
+    const int tiles = g.M / NC, clusters = tiles * g.ny * g.nz;
+    const int ticket = sp_begin(a.sync, clusters, bc);
+    const unsigned gen = bc[1];
     const int cl = ticket / F, f = ticket % F, fb = f * FB;
     const int tl = cl % tiles, yz = cl / tiles;
     const int y = yz % g.ny, z = yz / g.ny;
@@ -1799,13 +1847,11 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
     const int NS0 = tail0 ? PF : (K0 + 4 * PF - 1) / (4 * PF) * PF;
     const float* __restrict__ P = g.params + (long long)slot * g.P + (long long)y * g.ens;
     const rsrc_t rW = make_rsrc(P, g.P);
-    float* const X = a.sync.xch + (long long)cl * SP_CLUSTER_STRIDE;
-    const rsrc_t rX = make_rsrc(X, SP_CLUSTER_FLOATS);
-    unsigned* const cnt = a.sync.cnt + (long long)cl * SP_CNT_STRIDE;
-    unsigned npub = 0;  // hand-offs published by every block of the cluster so far
+    unsigned long long* const X = a.sync.xch + (long long)cl * SP_CLUSTER_GRANULES;
+    const rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)(SP_CLUSTER_GRANULES * 8), 0x00020000);
+    unsigned phase = 0;  // hand-offs of this launch so far
     const bool st = c0 >= g.st_lo && c0 + NC <= g.st_hi;
     const long long sbase = (long long)slot * g.s_ss + (long long)y * g.s_sy + c0;
-    // head A fragments of the block's unsplit waves (Euler: used every step)
     load_in0<NT>(in0, g.x0 + (long long)slot * g.x0_ss, K0, g.ld_x, c0);
     __syncthreads();
 
@@ -1819,45 +1865,47 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
         }
         ln_stats(S1, S2, (float)H, mean, rs);
     };
-    // normalise the slab in place (thread: features 2 tid, 2 tid + 1) with the statistics in stat[]
-    auto ln_slab = [&](int l) {
-        const float2 ga = *reinterpret_cast<const float2*>(&P[g.g_off[l] + 2 * tid]);
-        const float2 be = *reinterpret_cast<const float2*>(&P[g.be_off[l] + 2 * tid]);
+    // normalise the fragment-order slab in place with stat[] and lng[] (thread: 8 float4)
+    auto ln_slab = [&]() {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const float gv = h ? ga.y : ga.x, bv = h ? be.y : be.x;
-            float* row = &slab[(2 * tid + h) * NC];
-#pragma unroll
-            for (int c = 0; c < NC; ++c) row[c] = ln_apply(row[c], stat[0][c], stat[1][c], gv, bv);
+        for (int i = 0; i < 8; ++i) {
+            const int f4 = tid * 8 + i, gq = f4 >> 6, ln = f4 & 63, col = ln & 15, kk = ln >> 4;
+            float4 v = reinterpret_cast<float4*>(slab)[f4];
+            const float m = stat[0][col], r = stat[1][col];
+            v.x = ln_apply(v.x, m, r, lng[0][16 * gq + kk], lng[1][16 * gq + kk]);
+            v.y = ln_apply(v.y, m, r, lng[0][16 * gq + 4 + kk], lng[1][16 * gq + 4 + kk]);
+            v.z = ln_apply(v.z, m, r, lng[0][16 * gq + 8 + kk], lng[1][16 * gq + 8 + kk]);
+            v.w = ln_apply(v.w, m, r, lng[0][16 * gq + 12 + kk], lng[1][16 * gq + 12 + kk]);
+            reinterpret_cast<float4*>(slab)[f4] = v;
         }
     };
-    // the block's feature slice of a layer output in the slab -> G (and the LN stats -> MU / RS)
-    auto store_slab_slice = [&](int l) {
+    // layer outputs in the slab (features [k0, k0 + nk)) -> G [feature][ld_s]
+    auto store_slab_rows = [&](int l, int k0, int nk) {
         if (!st || g.G[l] == nullptr || c0 + NC > g.g_hi) return;
         float* Gp = g.G[l] + sbase;
-        for (int e = tid; e < FB * NC / 4; e += NT) {
-            const int fr = fb + e / (NC / 4), c4 = (e % (NC / 4)) * 4;
-            *reinterpret_cast<float4*>(&Gp[(long long)fr * g.ld_s + c4]) = *reinterpret_cast<const float4*>(&slab[fr * NC + c4]);
+        for (int e = tid; e < nk * NC; e += NT) {
+            const int k = k0 + e / NC, col = e % NC;
+            Gp[(long long)k * g.ld_s + col] = slab[sp_fidx(k, col)];
         }
     };
     auto store_stats = [&](int l) {
-        if (LN && st && f == 0 && tid < NC && g.MU[l]) {
+        if (LN && st && tid < NC && g.MU[l]) {
             const long long so = (long long)slot * g.st_ss + (long long)y * g.st_sy + c0 + tid;
             g.MU[l][so] = stat[0][tid];
             g.RS[l][so] = stat[1][tid];
         }
     };
-    // stage a published layer output (+ LN partials) from the exchange into the slab
-    auto stage = [&](int par) {
-#pragma unroll
-        for (int i = 0; i < (int)(SP_XB / 4 / NT); ++i) {
-            const int e = tid + i * NT;
-            reinterpret_cast<float4*>(slab)[e] = sp_load4(rX, (int)((par * SP_XB) * 4) + e * 16);
+    // stage a published layer output (+ LN partials, scale and bias of layer l) into the slab
+    auto stage = [&](int par, unsigned tag, int l) {
+        if (LN) {
+            lng[0][tid] = P[g.g_off[l] + tid];
+            lng[0][tid + NT] = P[g.g_off[l] + tid + NT];
+            lng[1][tid] = P[g.be_off[l] + tid];
+            lng[1][tid + NT] = P[g.be_off[l] + tid + NT];
+            // the words hold [w][s][c] (tid < 256 = 8 x 2 x 16); lnred is [s][w][c]
+            lnred[(tid / NC) & 1][tid / (2 * NC)][tid % NC] = gx_get(X, SP_G_LP + par * 8 * 2 * NC + tid, tag, a.sync);
         }
-        if (LN) {  // the exchange holds [w][s][c] (tid < 256 = 8 x 2 x 16); lnred is [s][w][c]
-            const float v = sp_load1(rX, (int)((SP_LP + par * 8 * 2 * NC) * 4) + tid * 4);
-            lnred[(tid / NC) & 1][tid / (2 * NC)][tid % NC] = v;
-        }
+        gx_stage(rX, par * SP_XG, tag, slab, a.sync);
         __syncthreads();
         if (LN) {
             if (tid < NC) col_stats(tid, stat[0][tid], stat[1][tid]);
@@ -1929,24 +1977,25 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
                         be[e] = P[g.be_off[0] + 64 * w + 16 * lk + e];
                     }
                 }
+                // feature 64 w + 16 lk + 4 r + c, column li: fragment-order float4 over r
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 4; ++c) {
+                    float x[4];
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        float x = v[h][r][c];
-                        if constexpr (LN) x = ln_apply(x, mean, rs, ga[4 * r + c], be[4 * r + c]);
-                        slab[(64 * w + 16 * lk + 4 * r + c) * NC + li] = x;
+                    for (int r = 0; r < 4; ++r) {
+                        x[r] = v[h][r][c];
+                        if constexpr (LN) x[r] = ln_apply(x[r], mean, rs, ga[4 * r + c], be[4 * r + c]);
                     }
+                    reinterpret_cast<float4*>(slab)[(4 * w + lk) * 64 + c * 16 + li] = float4{x[0], x[1], x[2], x[3]};
+                }
             }
             if constexpr (LN) {
-                if (tid < NC) {
-                    col_stats(tid, stat[0][tid], stat[1][tid]);
-                }
+                if (tid < NC) col_stats(tid, stat[0][tid], stat[1][tid]);
             }
             __syncthreads();
             if (!EULER) {
-                store_slab_slice(0);
-                store_stats(0);
+                store_slab_rows(0, fb, FB);
+                if (f == 0) store_stats(0);
             }
         }
         // ---- hidden layers 1 .. L-1, split ----
@@ -1957,14 +2006,13 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
         for (int p = 0; p < SP_PF; ++p) ring[p] = sp_aload<TPW>(rW, (int)g.w_off[1] + 4 * p * H + lo);
         for (int l = 1; l < L; ++l) {
             if (l >= 2) {
-                sp_wait(a.sync, cnt, (unsigned)F * npub);
-                stage((l - 1) & 1);
+                stage((l - 1) & 1, sp_tag(gen, phase - 1), l - 1);
                 if constexpr (LN) {
-                    ln_slab(l - 1);
+                    ln_slab();
                     __syncthreads();
                     // (without LN the producers stored G_{l-1} themselves)
-                    store_slab_slice(l - 1);
-                    store_stats(l - 1);
+                    store_slab_rows(l - 1, fb, FB);
+                    if (f == 0) store_stats(l - 1);
                 }
             }
             f32x4 acc[TPW];
@@ -1979,11 +2027,12 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
             }
             const int wcur = (int)g.w_off[l], wnext = (int)g.w_off[l + 1 < L ? l + 1 : 1];
             asm volatile("" ::"s"(wcur), "s"(wnext));
-            sp_kloop<TPW>(acc, ring, rW, slab, H / 4, wcur, wnext, lo, lk, li);
+            sp_kloop<TPW>(acc, ring, rW, slab, H / 4, wcur, wnext, lo, lane);
             // epilogue: tile t, reg r: feature fb + 16 TPW q + TPW (4 lk + r) + t, column li
             const bool last = l == L - 1;
             const bool stU = st && g.U[l];
             const bool stG = !LN && st && g.G[l] && c0 + NC <= g.g_hi;
+            const unsigned tag = sp_tag(gen, phase);
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -1994,7 +2043,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
                     const float gv = gelu_fast(u);
                     if (stG) g.G[l][sbase + (long long)(fb + fl) * g.ld_s + li] = gv;
                     tile[fl * NC + li] = gv;
-                    if (!EULER || !last) sp_store1(rX, gv, (int)(((l & 1) * SP_XB + (long long)(fb + fl) * NC + li) * 4));
+                    if (!EULER || !last) gx_put(X, (l & 1) * SP_XG + sp_fidx(fb + fl, li), gv, tag);
                 }
             __syncthreads();  // tile complete
             if (LN && q < TPW) {
@@ -2006,8 +2055,8 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
                 s2 = lk_sum(s2);
                 if (lk == 0) {
                     const int w8 = f * TPW + q;
-                    sp_store1(rX, s1, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + li) * 4));
-                    sp_store1(rX, s2, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + NC + li) * 4));
+                    gx_put(X, SP_G_LP + ((l & 1) * 8 + w8) * 2 * NC + li, s1, tag);
+                    gx_put(X, SP_G_LP + ((l & 1) * 8 + w8) * 2 * NC + NC + li, s2, tag);
                 }
             }
             if (EULER && last && q < TPW) {
@@ -2024,31 +2073,19 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
                     hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(w5r[s], tile[(64 * q + 4 * s + lk) * NC + li], hacc, 0, 0, 0);
                 if (lk < 2) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        sp_store1(rX, hacc[r], (int)((SP_HP + (w8 * 8 + 4 * lk + r) * NC + li) * 4));
+                    for (int r = 0; r < 4; ++r) gx_put(X, SP_G_HP + (w8 * 8 + 4 * lk + r) * NC + li, hacc[r], tag);
                 }
             }
-            ++npub;
-            const unsigned before = sp_publish(cnt, &bc);
+            ++phase;
             if (!EULER && last) {
                 // the cluster's last arriver: stage the last hidden layer, store it, run the head
-                if (before != (unsigned)F * npub - 1) break;
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                stage(l & 1);
-                if constexpr (LN) ln_slab(l);
-                __syncthreads();
-                if (LN && st && g.G[l] && c0 + NC <= g.g_hi) {
-                    float* Gp = g.G[l] + sbase;
-                    for (int e = tid; e < H * NC / 4; e += NT) {
-                        const int fr = e / (NC / 4), c4 = (e % (NC / 4)) * 4;
-                        *reinterpret_cast<float4*>(&Gp[(long long)fr * g.ld_s + c4]) =
-                            *reinterpret_cast<const float4*>(&slab[fr * NC + c4]);
-                    }
-                }
-                if (LN && st && tid < NC && g.MU[l]) {
-                    const long long so = (long long)slot * g.st_ss + (long long)y * g.st_sy + c0 + tid;
-                    g.MU[l][so] = stat[0][tid];
-                    g.RS[l][so] = stat[1][tid];
+                if (!sp_last(a.sync, cl, F, bc)) break;
+                stage(l & 1, tag, l);
+                if constexpr (LN) {
+                    ln_slab();
+                    __syncthreads();
+                    store_slab_rows(l, 0, H);
+                    store_stats(l);
                 }
                 // head partials of all 8 unsplit waves (wave q: 2q, 2q + 1), stream_fwd_kernel's order
 #pragma unroll
@@ -2062,7 +2099,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
                     f32x4 hacc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                     for (int s = 0; s < 16; ++s)
-                        hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(w5r[s], slab[(64 * w8 + 4 * s + lk) * NC + li], hacc, 0, 0, 0);
+                        hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(w5r[s], slab[sp_fidx(64 * w8 + 4 * s + lk, li)], hacc, 0, 0, 0);
                     if (lk < 2) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) hred[w8][4 * lk + r][li] = hacc[r];
@@ -2081,12 +2118,12 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
         }
         if constexpr (EULER) {
             // every block: the 8 unsplit-wave head partials, summed in euler_flow_kernel's order
-            sp_wait(a.sync, cnt, (unsigned)F * npub);
+            const unsigned tag = sp_tag(gen, phase - 1);
             if (tid < a.A * NC) {
                 const int aa = tid / NC, j = tid % NC;
-                float v = sp_load1(rX, (int)((SP_HP + aa * NC + j) * 4));
+                float v = gx_get(X, SP_G_HP + aa * NC + j, tag, a.sync);
 #pragma unroll
-                for (int w8 = 1; w8 < EF_NW; ++w8) v += sp_load1(rX, (int)((SP_HP + (w8 * 8 + aa) * NC + j) * 4));
+                for (int w8 = 1; w8 < EF_NW; ++w8) v += gx_get(X, SP_G_HP + (w8 * 8 + aa) * NC + j, tag, a.sync);
                 v += P[g.b_off[L] + aa];
                 float* xp = &in0[(a.D + aa) * NC + j];
                 *xp = *xp + v / a.steps_f;
@@ -2104,6 +2141,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
         __syncthreads();
         if (tid == 0) a.probe[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     }
+    sp_end(a.sync, clusters, clusters * F);
 }
 
 void launch_split_fwd(int head_mode, bool ln, bool euler, int F, const SplitFwdArgs& a, hipStream_t s) {
@@ -2116,11 +2154,13 @@ void launch_split_fwd(int head_mode, bool ln, bool euler, int F, const SplitFwdA
         default: FQ_SPF(MODE, LNV, EU, 4); break;        \
     }
     if (euler) {
-        FQ_SPF_T(HEAD_EULER, false, true)
+        if (F == 8) FQ_SPF(HEAD_EULER, false, true, 1);
+        else FQ_SPF(HEAD_EULER, false, true, 2);
     } else {
         switch (head_mode) {
-            case HEAD_BC_FUSED: if (ln) { FQ_SPF_T(HEAD_BC_FUSED, true, false) } else { FQ_SPF_T(HEAD_BC_FUSED, false, false) } break;
-            case HEAD_OS: if (ln) { FQ_SPF_T(HEAD_OS, true, false) } else { FQ_SPF_T(HEAD_OS, false, false) } break;
+            // (the actors have no LayerNorm: actor_layer_norm is refused at create)
+            case HEAD_BC_FUSED: FQ_SPF_T(HEAD_BC_FUSED, false, false) break;
+            case HEAD_OS: FQ_SPF_T(HEAD_OS, false, false) break;
             default: if (ln) { FQ_SPF_T(HEAD_STORE, true, false) } else { FQ_SPF_T(HEAD_STORE, false, false) } break;
         }
     }
@@ -2754,16 +2794,16 @@ void launch_stream_bwd(bool ln, const StreamBwdArgs& a, hipStream_t s) {
 
 // ============================================ split streamed backward (small populations) ==
 // stream_bwd_kernel with each 16-column tile computed by a cluster of F = 2, 4 or 8 blocks
-// (the split streamed forward's scheme): block f owns the 512/F features [fb, fb + 512/F) of
-// every dh_l / du_l; its 4 waves run TPW = 8/F 16x16 tiles of the dX products over the full
-// K (the unsplit k order, W_l^T rows as the A fragments), so every value is the unsplit fp32
-// chain.  The sums over features (LayerNorm backward column statistics) and over columns
-// (bias / LN / head-kernel grad partials) are re-done from LDS images of the block's
-// features in the unsplit order and lane layout ("unsplit wave" w = f TPW + q), so the
-// results are bit-identical to stream_bwd_kernel's.  Hand-offs per layer: the LN column
-// partials (LN only), then du_l (B operand of the next product, staged from the exchange).
-// The critic's dQ/da (columns >= Mg, layer 0) is computed by the cluster's last arriver
-// from the staged du_0, in the unsplit order.
+// (the split streamed forward's scheme and hand-off): block f owns the 512/F features
+// [fb, fb + 512/F) of every dh_l / du_l; its 4 waves run TPW = 8/F 16x16 tiles of the dX
+// products over the full K (the unsplit k order, W_l^T rows as the A fragments, du_l from the
+// fragment-order slab), so every value is the unsplit fp32 chain.  The sums over features
+// (LayerNorm backward column statistics) and over columns (bias / LN / head-kernel grad
+// partials) are re-done from LDS images of the block's features in the unsplit order and
+// lane layout ("unsplit wave" w = f TPW + q), so the results are bit-identical to
+// stream_bwd_kernel's.  Hand-offs per layer: the LN column partials (LN only), then du_l
+// (the next product's B operand).  The critic's dQ/da (columns >= Mg, layer 0) is computed
+// by the cluster's last arriver from the staged du_0, in the unsplit order.
 bool split_bwd_supported(int H, int L, int nout, int M, int Mg) {
     return H == EF_H && L >= 2 && L <= EF_MAX_LAYERS && nout >= 1 && nout <= 8 && M % EF_NC == 0 &&
            Mg % EF_NC == 0 && Mg <= M;
@@ -2771,16 +2811,17 @@ bool split_bwd_supported(int H, int L, int nout, int M, int Mg) {
 
 template <bool LN, int TPW>
 __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs g, const SplitSync sync) {
-    constexpr int H = EF_H, NC = EF_NC, NT = SP_NT, F = 8 / TPW, FB = H / F;
-    __shared__ __attribute__((aligned(16))) float slab[H * NC + 64];   // du_l [H][NC] (+ look-ahead slack)
+    constexpr int H = EF_H, NC = EF_NC, F = 8 / TPW, FB = H / F;
+    __shared__ __attribute__((aligned(16))) float slab[H * NC + 256];  // du_l, fragment order (+ slack)
     __shared__ __attribute__((aligned(16))) float ta[FB * NC];          // the block's dh (raw), then du
     __shared__ __attribute__((aligned(16))) float tb[FB * NC];          // the block's xhat (LN)
     __shared__ float cst[2][NC];                                        // c1, c2 per column
     __shared__ float dos[8][NC];
-    __shared__ unsigned bc;
+    __shared__ unsigned bc[2];
 
-    const int tiles = g.M / NC;
-    const int ticket = sp_ticket(sync, tiles * g.ny * g.nz, &bc);
+    const int tiles = g.M / NC, clusters = tiles * g.ny * g.nz;
+    const int ticket = sp_begin(sync, clusters, bc);
+    const unsigned gen = bc[1];
     const int cl = ticket / F, f = ticket % F, fb = f * FB;
     const int tl = cl % tiles, yz = cl / tiles;
     const int y = yz % g.ny, z = yz / g.ny;
@@ -2798,10 +2839,9 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
     const long long sto = (long long)slot * g.st_ss + (long long)y * g.st_sy + g.coff + c0;
     const long long dso = (long long)slot * g.d_ss + (long long)y * g.d_sy + c0;
     float* __restrict__ part = gp ? g.part + ((long long)(slot * g.ny + y) * (g.Mg / NC) + tl) * g.NP : nullptr;
-    float* const X = sync.xch + (long long)cl * SP_CLUSTER_STRIDE;
-    const rsrc_t rX = make_rsrc(X, SP_CLUSTER_FLOATS);
-    unsigned* const cnt = sync.cnt + (long long)cl * SP_CNT_STRIDE;
-    unsigned npub = 0;
+    unsigned long long* const X = sync.xch + (long long)cl * SP_CLUSTER_GRANULES;
+    const rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)(SP_CLUSTER_GRANULES * 8), 0x00020000);
+    unsigned phase = 0;
     const int w5 = (LN ? 3 : 1) * L * H;
     // lane layout: tile t, reg r -> feature fb + fl, fl = 16 TPW q + TPW (4 lk + r) + t, column li
     auto flo = [&](int r, int t) { return 16 * TPW * q + TPW * (4 * lk + r) + t; };
@@ -2876,10 +2916,8 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
 
     float4 ring[SP_PF];
     const int lo = lk * H + fb + 16 * TPW * q + TPW * li;
-    if (L >= 2) {
 #pragma unroll
-        for (int p = 0; p < SP_PF; ++p) ring[p] = sp_aload<TPW>(rT, (int)g.wt_off[L - 1] + 4 * p * H + lo);
-    }
+    for (int p = 0; p < SP_PF; ++p) ring[p] = sp_aload<TPW>(rT, (int)g.wt_off[L - 1] + 4 * p * H + lo);
     for (int l = L - 1; l >= 0; --l) {
         // epilogue inputs of layer l (own features)
         float u[4][TPW];
@@ -2901,6 +2939,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
                     tb[flo(r, t) * NC + li] = xh[r][t];
                 }
             __syncthreads();
+            const unsigned tag = sp_tag(gen, phase);
             if (q < TPW) {
                 // unsplit wave w8 = f TPW + q: LN bias grads (reduce-scatter of dh), column partials of
                 // dh gamma and dh gamma xhat (16 consecutive features per lane, then the lk sum)
@@ -2917,8 +2956,8 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
                 s1 = lk_sum(s1);
                 s2 = lk_sum(s2);
                 if (lk == 0) {
-                    sp_store1(rX, s1, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + li) * 4));
-                    sp_store1(rX, s2, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + NC + li) * 4));
+                    gx_put(X, SP_G_LP + ((l & 1) * 8 + w8) * 2 * NC + li, s1, tag);
+                    gx_put(X, SP_G_LP + ((l & 1) * 8 + w8) * 2 * NC + NC + li, s2, tag);
                 }
             }
             if (gp && tid < FB) {
@@ -2933,15 +2972,13 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
                 }
                 part[(L + l) * H + fb + tid] = sv;
             }
-            ++npub;
-            sp_publish(cnt, &bc);
-            sp_wait(sync, cnt, (unsigned)F * npub);
+            ++phase;
             if (tid < NC) {
                 float c1 = 0.f, c2 = 0.f;
 #pragma unroll
                 for (int w8 = 0; w8 < EF_NW; ++w8) {
-                    c1 += sp_load1(rX, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + tid) * 4));
-                    c2 += sp_load1(rX, (int)((SP_LP + ((l & 1) * 8 + w8) * 2 * NC + NC + tid) * 4));
+                    c1 += gx_get(X, SP_G_LP + ((l & 1) * 8 + w8) * 2 * NC + tid, tag, sync);
+                    c2 += gx_get(X, SP_G_LP + ((l & 1) * 8 + w8) * 2 * NC + NC + tid, tag, sync);
                 }
                 cst[0][tid] = c1 / (float)H;
                 cst[1][tid] = c2 / (float)H;
@@ -2963,6 +3000,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
         }
         // du_l: DU (dW operand), the LDS image (bias grads), the exchange (next product / dQ/da)
         const bool need_x = l > 0 || (g.da != nullptr && !gp);
+        const unsigned tag = sp_tag(gen, phase);
         __syncthreads();  // ta is free (LN: read above)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -2971,23 +3009,17 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
                 const int fl = flo(r, t);
                 if (gp || g.da == nullptr) g.DU[l][dso + (long long)(fb + fl) * g.ld_d + li] = dh[r][t];
                 ta[fl * NC + li] = dh[r][t];
-                if (need_x) sp_store1(rX, dh[r][t], (int)((((l & 1) * SP_XB) + (long long)(fb + fl) * NC + li) * 4));
+                if (need_x) gx_put(X, (l & 1) * SP_XG + sp_fidx(fb + fl, li), dh[r][t], tag);
             }
         __syncthreads();
         if (gp && tid < FB) part[l * H + fb + tid] = row_sum(ta, tid);  // bias: sum du
         if (!need_x) break;
-        ++npub;
-        const unsigned before = sp_publish(cnt, &bc);
+        ++phase;
         if (l == 0) {
             // dQ/da of the Q-loss columns by the cluster's last arriver (stream_bwd_kernel's order:
             // 4 feature quarters of W_0[D0 + j][f] du_0[f][col], then their sum in quarter order)
-            if (before != (unsigned)F * npub - 1) break;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int i = 0; i < (int)(SP_XB / 4 / NT); ++i) {
-                const int e = tid + i * NT;
-                reinterpret_cast<float4*>(slab)[e] = sp_load4(rX, e * 16);  // du_0 (exchange parity 0)
-            }
+            if (!sp_last(sync, cl, F, bc)) break;
+            gx_stage(rX, 0, tag, slab, sync);  // du_0 (exchange parity 0)
             __syncthreads();
             float* const scr = tb;  // [4 quarters][128] (FB NC >= 1024 floats)
 #pragma unroll
@@ -2997,7 +3029,8 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
                 if (j < g.na) {
                     const float* wr = P + g.w_off[0] + (long long)(g.D0 + j) * H;
 #pragma unroll 8
-                    for (int fe = qd * (H / 4); fe < (qd + 1) * (H / 4); ++fe) sacc = fmaf(wr[fe], slab[fe * NC + col], sacc);
+                    for (int fe = qd * (H / 4); fe < (qd + 1) * (H / 4); ++fe)
+                        sacc = fmaf(wr[fe], slab[sp_fidx(fe, col)], sacc);
                 }
                 scr[qd * 128 + o] = sacc;
             }
@@ -3008,23 +3041,19 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
             break;
         }
         // ---- dh_{l-1} = W_l du_l over the staged du_l (all 512 features) ----
-        sp_wait(sync, cnt, (unsigned)F * npub);
-#pragma unroll
-        for (int i = 0; i < (int)(SP_XB / 4 / NT); ++i) {
-            const int e = tid + i * NT;
-            reinterpret_cast<float4*>(slab)[e] = sp_load4(rX, (int)(((l & 1) * SP_XB) * 4) + e * 16);
-        }
+        gx_stage(rX, (l & 1) * SP_XG, tag, slab, sync);
         __syncthreads();
         f32x4 acc[TPW];
 #pragma unroll
         for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int wn = (int)g.wt_off[l >= 2 ? l - 1 : l];
-        sp_kloop<TPW>(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lo, lk, li);
+        sp_kloop<TPW>(acc, ring, rT, slab, H / 4, (int)g.wt_off[l], wn, lo, lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int t = 0; t < TPW; ++t) dh[r][t] = acc[t][r];
     }
+    sp_end(sync, clusters, clusters * F);
 }
 
 void launch_split_bwd(bool ln, int F, const StreamBwdArgs& a, const SplitSync& sy, hipStream_t s) {
@@ -3033,7 +3062,7 @@ void launch_split_bwd(bool ln, int F, const StreamBwdArgs& a, const SplitSync& s
     switch (F) {
         case 8: if (ln) FQ_SPB(true, 1); else FQ_SPB(false, 1); break;
         case 4: if (ln) FQ_SPB(true, 2); else FQ_SPB(false, 2); break;
-        default: if (ln) FQ_SPB(true, 4); else FQ_SPB(false, 4); break;
+        default: FQ_SPB(false, 4); break;  // (the LN backward runs 4 or 8 blocks per tile)
     }
 #undef FQ_SPB
 }

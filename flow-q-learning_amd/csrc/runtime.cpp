@@ -253,8 +253,9 @@ struct fqlpop {
     // split launches (engine option split): per launch site an exchange area and a block of
     // arrival counters (zeroed by a memset node before every launch), and one error word
     struct SplitSite {
-        float* xch = nullptr;
+        unsigned long long* xch = nullptr;
         unsigned* cnt = nullptr;
+        unsigned* gen = nullptr;
         long long clusters = 0;    // capacity
     } split_site[7];
     unsigned* split_err = nullptr;
@@ -559,21 +560,21 @@ constexpr long long kSplitMaxBlocks = 256;    // one block per CU (see split_fac
 int split_factor(const fqlpop* h, long long clusters, bool min4, long long max_blocks = kSplitMaxBlocks) {
     const int opt = h->opt.split;
     if (!h->split_ok || opt == 0 || clusters > kSplitMaxClusters) return 1;
-    for (int F = opt >= 2 ? opt : 8; F >= 2; F /= 2) {
+    for (int F = std::max(opt >= 2 ? opt : 8, min4 ? 4 : 2); F >= 2; F /= 2) {
         if (min4 && F < 4) break;
         if (clusters * F <= max_blocks) return F;
     }
     return 1;
 }
 
-// The site's synchronisation state for one launch over `clusters` tiles: its arrival counters
-// and the ticket counter after them are zeroed on `s` first (a memset node in the step's
-// graph).
+// The site's synchronisation state for one launch over `clusters` tiles: its counters (per
+// cluster, then the ticket and the exit counter) are zeroed on `s` first (a memset node in the
+// step's graph).
 SplitSync split_prep(fqlpop* h, int site, long long clusters, hipStream_t s) {
     fqlpop::SplitSite& st = h->split_site[site];
     ARGCHK(clusters <= st.clusters, "split launch larger than its site");
-    HIPCHK(hipMemsetAsync(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (clusters + 1), s));
-    return SplitSync{st.xch, st.cnt, h->split_err};
+    HIPCHK(hipMemsetAsync(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (clusters + 2), s));
+    return SplitSync{st.xch, st.cnt, st.gen, h->split_err};
 }
 
 // Blocks per tile of a streamed backward launch (1 = unsplit): the critic (LN: its 2-block
@@ -1751,9 +1752,12 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             for (int si = 0; si < SITE_N; ++si) {
                 auto& st = h->split_site[si];
                 st.clusters = std::min(kSplitMaxClusters, tiles_per_member[si] * n);
-                HIPCHK(hipMalloc(&st.xch, sizeof(float) * split_cluster_floats() * st.clusters));
-                HIPCHK(hipMalloc(&st.cnt, sizeof(unsigned) * split_counter_stride() * (st.clusters + 1)));
-                HIPCHK(hipMemset(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (st.clusters + 1)));
+                HIPCHK(hipMalloc(&st.xch, split_cluster_bytes() * st.clusters));
+                HIPCHK(hipMemset(st.xch, 0, split_cluster_bytes() * st.clusters));  // tag 0 matches no hand-off
+                HIPCHK(hipMalloc(&st.cnt, sizeof(unsigned) * split_counter_stride() * (st.clusters + 2)));
+                HIPCHK(hipMemset(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (st.clusters + 2)));
+                HIPCHK(hipMalloc(&st.gen, 64));
+                HIPCHK(hipMemset(st.gen, 0, 64));
             }
             HIPCHK(hipMalloc(&h->split_err, 64));
             HIPCHK(hipMemset(h->split_err, 0, 64));
@@ -1810,6 +1814,7 @@ int fqlpop_destroy(fqlpop_t* h) {
         for (auto& st : h->split_site) {
             if (st.xch) (void)hipFree(st.xch);
             if (st.cnt) (void)hipFree(st.cnt);
+            if (st.gen) (void)hipFree(st.gen);
         }
         if (h->split_err) (void)hipFree(h->split_err);
         for (hipEvent_t e : {h->ev_sample, h->ev_bcfwd, h->ev_bcloss, h->ev_flow, h->ev_bdone, h->ev_t0, h->ev_t1})
