@@ -195,7 +195,8 @@ void launch_stream_fwd(int head_mode, bool ln, const StreamArgs& a, hipStream_t 
 struct SplitSync {
     unsigned long long* xch;  // exchange words {value, tag}, split_cluster_bytes() per cluster
     unsigned* cnt;            // counters split_counter_stride() apart: [clusters] last-arriver, then the
-                              // ticket and the exit counter; zeroed before every launch
+                              // ticket and the exit counter; zero at launch (the last block of every
+                              // launch zeroes them)
     unsigned* gen;            // the site's launch generation (never zeroed; the tags' high bits)
     unsigned* err;            // set to nonzero when a hand-off wait gives up (results then invalid)
 };

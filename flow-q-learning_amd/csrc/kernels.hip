@@ -1653,8 +1653,9 @@ void launch_stream_fwd(int head_mode, bool ln, const StreamArgs& a, hipStream_t 
 //     sums the 8 in the unsplit order (x += v / S for the next step); the forward's head is
 //     computed by the cluster's LAST arriver (told by its add to the cluster's counter), which
 //     stages the last hidden layer, stores its G (and LN statistics) and calls head_write.
-// The counters (cluster, ticket, exit) are zeroed by a memset node before every launch; spins
-// give up after ~2 s and set sync.err (the runtime then reports an error instead of hanging).
+// The counters (cluster, ticket, exit) are zeroed by the last block to exit each launch (and
+// at allocation, and by the runtime after an error); spins give up after ~2 s and set
+// sync.err (the runtime then reports an error instead of hanging).
 // Residency: a block takes its (cluster, slice) from a launch-wide ticket counter when it
 // starts (sp_begin), so clusters are formed in the order blocks become resident: at any time
 // a launch has at most one cluster whose blocks are not all resident, and every other cluster
@@ -1693,13 +1694,19 @@ DEV int sp_begin(const SplitSync& sy, int clusters, unsigned* bc) {
     __syncthreads();
     return (int)bc[0];
 }
-// block end (every block, every path): the last one to exit advances the site's generation
-DEV void sp_end(const SplitSync& sy, int clusters, int blocks) {
+// block end (every block, every path): the last one to exit advances the site's generation and
+// zeroes the launch's counters (every other block has taken its ticket, made its last-arriver
+// add and exited), so the next launch of the site needs no memset node
+DEV void sp_end(const SplitSync& sy, int clusters, int blocks, unsigned* bc) {
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned e = __hip_atomic_fetch_add((gu32_t*)(sy.cnt + (long long)(clusters + 1) * SP_CNT_STRIDE), 1u,
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (e == (unsigned)blocks - 1) __hip_atomic_fetch_add((gu32_t*)sy.gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0)
+        bc[0] = __hip_atomic_fetch_add((gu32_t*)(sy.cnt + (long long)(clusters + 1) * SP_CNT_STRIDE), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (bc[0] == (unsigned)blocks - 1) {
+        for (int c = threadIdx.x; c < clusters + 2; c += blockDim.x)
+            __hip_atomic_store((gu32_t*)(sy.cnt + (long long)c * SP_CNT_STRIDE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32_t*)sy.gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 DEV unsigned sp_tag(unsigned gen, unsigned phase) { return (gen << 8) | ((phase + 1) & 255u); }
@@ -2141,7 +2148,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
         __syncthreads();
         if (tid == 0) a.probe[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     }
-    sp_end(a.sync, clusters, clusters * F);
+    sp_end(a.sync, clusters, clusters * F, bc);
 }
 
 void launch_split_fwd(int head_mode, bool ln, bool euler, int F, const SplitFwdArgs& a, hipStream_t s) {
@@ -3053,7 +3060,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
 #pragma unroll
             for (int t = 0; t < TPW; ++t) dh[r][t] = acc[t][r];
     }
-    sp_end(sync, clusters, clusters * F);
+    sp_end(sync, clusters, clusters * F, bc);
 }
 
 void launch_split_bwd(bool ln, int F, const StreamBwdArgs& a, const SplitSync& sy, hipStream_t s) {

@@ -567,13 +567,13 @@ int split_factor(const fqlpop* h, long long clusters, bool min4, long long max_b
     return 1;
 }
 
-// The site's synchronisation state for one launch over `clusters` tiles: its counters (per
-// cluster, then the ticket and the exit counter) are zeroed on `s` first (a memset node in the
-// step's graph).
-SplitSync split_prep(fqlpop* h, int site, long long clusters, hipStream_t s) {
+// The site's synchronisation state for one launch over `clusters` tiles.  Its counters (per
+// cluster, then the ticket and the exit counter) are zero at every launch: zeroed at
+// allocation, by the last block of every launch, and by check_split_error after a failed one
+// (no memset node in the step: at 2 members the seven 5-8 us fills were on the chains).
+SplitSync split_prep(fqlpop* h, int site, long long clusters, hipStream_t) {
     fqlpop::SplitSite& st = h->split_site[site];
     ARGCHK(clusters <= st.clusters, "split launch larger than its site");
-    HIPCHK(hipMemsetAsync(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (clusters + 2), s));
     return SplitSync{st.xch, st.cnt, st.gen, h->split_err};
 }
 
@@ -1526,6 +1526,8 @@ void check_split_error(fqlpop* h) {
     HIPCHK(hipMemcpy(&e, h->split_err, sizeof(e), hipMemcpyDeviceToHost));
     if (e != 0) {
         HIPCHK(hipMemset(h->split_err, 0, sizeof(e)));
+        for (auto& st : h->split_site)  // a launch that gave up may have left its counters set
+            if (st.cnt) HIPCHK(hipMemset(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (st.clusters + 2)));
         throw FqErr{FQLPOP_E_STATE, "a split launch's hand-off wait timed out (blocks of a cluster not resident "
                                     "together); results of the last steps are invalid"};
     }
