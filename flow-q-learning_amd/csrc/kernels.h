@@ -208,6 +208,7 @@ struct SplitFwdArgs {
     float steps_f;
     unsigned long long* probe;   // optional per-block {start, end} stamps
     SplitSync sync;
+    unsigned long long* phase;   // diagnostics (FQLPOP_PHASE_PROBE, Euler): [EF_PHASE_STRIDE] per block
 };
 long long split_cluster_bytes();
 int split_counter_stride();

@@ -1783,13 +1783,21 @@ DEV float4 sp_aload(rsrc_t r, int elem_off) {
 
 // One split hidden layer's k-loop (see ef_kloop): acc[t] += W[k][col + t] x[k][li] over the
 // NS k-steps, B from the fragment-order slab (one float4 = 4 k-steps, read a group ahead);
-// ring[] holds this layer's first SP_PF k-steps on entry and the next layer's (w_next) on
-// exit.  lo = lk * H + col.
-constexpr int SP_PF = 8;
+// ring[] holds this layer's first sp_pf<TPW> k-steps on entry and the next layer's (w_next)
+// on exit.  lo = lk * H + col.
+// Prefetch depth: a k-step issues TPW dependent-latency MFMAs (40 cycles each), so an 8-deep
+// ring covers only 320 cycles at TPW = 1, less than one Infinity-Cache hit (545 cycles idle,
+// more under load): the ring holds SP_PFW / TPW k-steps (the same SP_PFW VGPRs at every TPW).
+#ifndef FQ_SP_PFW
+#define FQ_SP_PFW 32
+#endif
+constexpr int SP_PFW = FQ_SP_PFW;
 template <int TPW>
-DEV void sp_kloop(f32x4 (&acc)[TPW], float4 (&ring)[SP_PF], rsrc_t rW, const float* xs, int NS, int w_cur,
+constexpr int sp_pf() { return SP_PFW / TPW < 8 ? 8 : SP_PFW / TPW; }
+template <int TPW, int PF = sp_pf<TPW>()>
+DEV void sp_kloop(f32x4 (&acc)[TPW], float4 (&ring)[PF], rsrc_t rW, const float* xs, int NS, int w_cur,
                   int w_next, int lo, int lane) {
-    constexpr int H = EF_H, PF = SP_PF;
+    constexpr int H = EF_H;
     const float4* x4 = reinterpret_cast<const float4*>(xs);
     float4 bn = x4[lane], b4 = bn;
     int s0 = 0;
@@ -1850,6 +1858,23 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
     const int li = lane & 15, lk = lane >> 4;
     const int L = g.L, K0 = g.K0, nout = g.head.nout;
     if (a.probe != nullptr && tid == 0) a.probe[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#ifdef FQ_PHASE_PROBE  // diagnostic build only (make PHASE=1): the Euler flow's per-layer phases
+    // [0] start, [1] inputs loaded; step st, layer l: 1 + 4 (st (L + 1) + l) + {0 layer start,
+    // 1 input staged, 2 k-loop end, 3 published}; head (l = L): {0 start, 3 state updated};
+    // [STRIDE - 1] XCC_ID, [STRIDE - 2] HW_ID, [STRIDE - 3] ticket
+    unsigned long long* const ph = EULER && a.phase != nullptr ? a.phase + (long long)blockIdx.x * EF_PHASE_STRIDE : nullptr;
+    auto stamp = [&](int st, int l, int i) {
+        if (ph != nullptr && tid == 0) ph[st < 0 ? i : 1 + 4 * (st * (L + 1) + l) + i] = __builtin_amdgcn_s_memrealtime();
+    };
+    if (ph != nullptr && tid == 0) {
+        ph[EF_PHASE_STRIDE - 1] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
+        ph[EF_PHASE_STRIDE - 2] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+        ph[EF_PHASE_STRIDE - 3] = (unsigned)ticket;
+    }
+    stamp(-1, 0, 0);
+#else
+    auto stamp = [](int, int, int) {};
+#endif
     const bool tail0 = K0 > 4 * PF && K0 <= 4 * (PF + 1);
     const int NS0 = tail0 ? PF : (K0 + 4 * PF - 1) / (4 * PF) * PF;
     const float* __restrict__ P = g.params + (long long)slot * g.P + (long long)y * g.ens;
@@ -1861,6 +1886,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
     const long long sbase = (long long)slot * g.s_ss + (long long)y * g.s_sy + c0;
     load_in0<NT>(in0, g.x0 + (long long)slot * g.x0_ss, K0, g.ld_x, c0);
     __syncthreads();
+    stamp(-1, 0, 1);
 
     // LayerNorm statistics of one column from the 8 unsplit-wave partials (stream_fwd_kernel's sums)
     auto col_stats = [&](int col, float& mean, float& rs) {
@@ -1926,7 +1952,11 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
             if (tid < NC) in0[(a.D + a.A) * NC + tid] = (float)((double)step / (double)a.S);
             __syncthreads();
         }
+        const int pst = step - a.first;  // (phase stamps)
+        (void)pst;
         // ---- layer 0, redundantly in every block: unsplit waves 2q, 2q + 1 ----
+        stamp(pst, 0, 0);
+        stamp(pst, 0, 1);
         {
             float v[2][4][4];
 #pragma unroll
@@ -1971,6 +2001,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
                 }
             }
             __syncthreads();  // lnred visible; every wave is done reading the slab (previous layer)
+            stamp(pst, 0, 2);
             float mean = 0.f, rs = 0.f;
             if constexpr (LN) col_stats(li, mean, rs);
 #pragma unroll
@@ -2004,14 +2035,18 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
                 store_slab_rows(0, fb, FB);
                 if (f == 0) store_stats(0);
             }
+            stamp(pst, 0, 3);
         }
         // ---- hidden layers 1 .. L-1, split ----
-        float4 ring[SP_PF];
+        // (the Euler flow at TPW = 2 keeps the 8-deep ring: a deeper one spills)
+        constexpr int RPF = EULER && TPW == 2 ? 8 : sp_pf<TPW>();
+        float4 ring[RPF];
         const int col = fb + 16 * TPW * q + TPW * li;
         const int lo = lk * H + col;
 #pragma unroll
-        for (int p = 0; p < SP_PF; ++p) ring[p] = sp_aload<TPW>(rW, (int)g.w_off[1] + 4 * p * H + lo);
+        for (int p = 0; p < RPF; ++p) ring[p] = sp_aload<TPW>(rW, (int)g.w_off[1] + 4 * p * H + lo);
         for (int l = 1; l < L; ++l) {
+            stamp(pst, l, 0);
             if (l >= 2) {
                 stage((l - 1) & 1, sp_tag(gen, phase - 1), l - 1);
                 if constexpr (LN) {
@@ -2034,7 +2069,9 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
             }
             const int wcur = (int)g.w_off[l], wnext = (int)g.w_off[l + 1 < L ? l + 1 : 1];
             asm volatile("" ::"s"(wcur), "s"(wnext));
-            sp_kloop<TPW>(acc, ring, rW, slab, H / 4, wcur, wnext, lo, lane);
+            stamp(pst, l, 1);
+            sp_kloop<TPW, RPF>(acc, ring, rW, slab, H / 4, wcur, wnext, lo, lane);
+            stamp(pst, l, 2);
             // epilogue: tile t, reg r: feature fb + 16 TPW q + TPW (4 lk + r) + t, column li
             const bool last = l == L - 1;
             const bool stU = st && g.U[l];
@@ -2084,6 +2121,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
                 }
             }
             ++phase;
+            stamp(pst, l, 3);
             if (!EULER && last) {
                 // the cluster's last arriver: stage the last hidden layer, store it, run the head
                 if (!sp_last(a.sync, cl, F, bc)) break;
@@ -2126,6 +2164,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
         if constexpr (EULER) {
             // every block: the 8 unsplit-wave head partials, summed in euler_flow_kernel's order
             const unsigned tag = sp_tag(gen, phase - 1);
+            stamp(pst, L, 0);
             if (tid < a.A * NC) {
                 const int aa = tid / NC, j = tid % NC;
                 float v = gx_get(X, SP_G_HP + aa * NC + j, tag, a.sync);
@@ -2138,6 +2177,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
                 in0[(a.D + a.A) * NC + tid - a.A * NC] = (float)((double)(step + 1) / (double)a.S);
             }
             __syncthreads();
+            stamp(pst, L, 3);
         }
     }
     if (EULER && f == 0 && tid < a.A * NC) {
@@ -2921,10 +2961,10 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
         return sv;
     };
 
-    float4 ring[SP_PF];
+    float4 ring[sp_pf<TPW>()];
     const int lo = lk * H + fb + 16 * TPW * q + TPW * li;
 #pragma unroll
-    for (int p = 0; p < SP_PF; ++p) ring[p] = sp_aload<TPW>(rT, (int)g.wt_off[L - 1] + 4 * p * H + lo);
+    for (int p = 0; p < sp_pf<TPW>(); ++p) ring[p] = sp_aload<TPW>(rT, (int)g.wt_off[L - 1] + 4 * p * H + lo);
     for (int l = L - 1; l >= 0; --l) {
         // epilogue inputs of layer l (own features)
         float u[4][TPW];

@@ -77,6 +77,11 @@ struct EngineOptions {
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
     int split = 1;         // small populations: streamed forwards / Euler flow as clusters of 2-8 blocks per
                            // 16-column tile (bit-identical); 0 off, 1 auto, 2 / 4 / 8 blocks where they fit
+    int small_sched = 1;   // small populations (the Euler flow split): target critic and the critic's
+                           // TD-column backward on a 4th stream beside the main chain (bit-identical)
+    int hw_queues = 4;     // the HIP runtime's hardware queues per process (GPU_MAX_HW_QUEUES, which the
+                           // caller sets; the Python layer passes it): below 4 the step is captured on
+                           // one stream (graph launch and hardware queues)
 };
 // (Schedule experiments that measured slower were removed in round 4 and stay in git history
 // and DESIGN.md section 5: a 4th stream, stream priorities, the critic optimiser on the main
@@ -98,6 +103,8 @@ const EngineOptionRef kEngineOptions[] = {
     {"dw_tile_actor", &EngineOptions::dw_tile_actor, 0, 10},
     {"adam_nt", &EngineOptions::adam_nt, 0, 3},
     {"split", &EngineOptions::split, 0, 8},
+    {"small_sched", &EngineOptions::small_sched, 0, 1},
+    {"hw_queues", &EngineOptions::hw_queues, 1, 1024},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -241,7 +248,7 @@ struct fqlpop {
     float *inj_batch = nullptr, *inj_noise = nullptr;
     long long inj_bs = 0, inj_ns = 0;
 
-    hipStream_t sM = nullptr, sF = nullptr, sB = nullptr;
+    hipStream_t sM = nullptr, sF = nullptr, sB = nullptr, sX = nullptr;  // sX: small-population schedule
     hipEvent_t ev_sample, ev_bcfwd, ev_bcloss, ev_flow, ev_bdone;
     hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;  // fqlpop_time_dominant_kernel
     std::vector<hipEvent_t> ev_pool;
@@ -257,7 +264,7 @@ struct fqlpop {
         unsigned* cnt = nullptr;
         unsigned* gen = nullptr;
         long long clusters = 0;    // capacity
-    } split_site[7];
+    } split_site[8];
     unsigned* split_err = nullptr;
     bool split_ok = false;
     bool stream_fwd = false;       // whole-network forward launches (stream_fwd_kernel)
@@ -545,7 +552,9 @@ void gemm(int layout, int epi, const GemmArgs& g, hipStream_t s) {
 // critic, critic forwards (sM).
 // critic and one-step backwards (sM).  The BC backward (sB) stays unsplit: at most two split
 // launches (one per stream of sF, sM) can then run at once.
-enum { SITE_BCF = 0, SITE_EULER = 1, SITE_OSF = 2, SITE_TGT = 3, SITE_CRF = 4, SITE_CRB = 5, SITE_OSB = 6, SITE_N = 7 };
+// (SITE_CRB2: the critic's TD-column backward on sX in the small-population schedule)
+enum { SITE_BCF = 0, SITE_EULER = 1, SITE_OSF = 2, SITE_TGT = 3, SITE_CRF = 4, SITE_CRB = 5, SITE_OSB = 6, SITE_CRB2 = 7,
+       SITE_N = 8 };
 constexpr long long kSplitMaxClusters = 128;  // a site with more 16-column tiles runs unsplit
 constexpr long long kSplitMaxBlocks = 256;    // one block per CU (see split_factor)
 
@@ -774,11 +783,13 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         const int F = bwd_split(h, N, M, Mg, c.nz);
         if (F > 1) {
             const long long clusters = (long long)(M / 16) * N.E * c.nz;
-            launch_split_bwd(N.ln, F, a, split_prep(h, &N == &h->critic ? SITE_CRB : SITE_OSB, clusters, s), s);
+            const int site = &N != &h->critic ? SITE_OSB : (s == h->sX && h->sX != h->sM) ? SITE_CRB2 : SITE_CRB;
+            launch_split_bwd(N.ln, F, a, split_prep(h, site, clusters, s), s);
         } else {
             launch_stream_bwd(N.ln, a, s);
         }
     }
+    if (Mg == 0) return;  // (the critic's Q-loss columns alone: no parameter grads)
     hipEvent_t ev = nullptr;
     if (sw != s) {
         ev = next_event(h);
@@ -987,6 +998,7 @@ SplitFwdArgs euler_split_args(fqlpop* h, const EulerArgs& ea, hipStream_t s) {
     sa.aflow = ea.aflow;
     sa.D = ea.D; sa.A = ea.A; sa.S = ea.S; sa.first = ea.first; sa.steps_f = ea.steps_f;
     sa.probe = ea.probe;
+    sa.phase = ea.phase;
     sa.sync = split_prep(h, SITE_EULER, (long long)(ea.B / 16) * ea.nz, s);
     return sa;
 }
@@ -1116,6 +1128,50 @@ void euler_phase_report(const unsigned long long* ph, long long nb, int L, int s
     std::fprintf(stderr, "  head per step: %.3f\n", kl[L] * per);
 }
 
+// FQLPOP_PHASE_PROBE, split Euler launch: mean per-step phases (us) over blocks and steps:
+// per hidden layer the wait for the previous layer's words (stage), the k-loop, the epilogue
+// + publish; the head's wait for the 8 partials; and the spread of the blocks' start times
+void split_euler_phase_report(const unsigned long long* ph, long long nb, int L, int steps) {
+    double stg[9] = {}, kl[9] = {}, ep[9] = {}, head = 0, pro = 0, blk = 0, l0 = 0;
+    long long n = 0, t0 = -1, t1 = 0, tl = 0;
+    int xcc[8] = {};
+    for (long long b = 0; b < nb; ++b) {
+        const unsigned long long* p = ph + b * EF_PHASE_STRIDE;
+        if (p[0] == 0) continue;
+        ++n;
+        t0 = t0 < 0 ? (long long)p[0] : std::min(t0, (long long)p[0]);
+        tl = std::max(tl, (long long)p[0]);
+        const unsigned long long* e = p + 1 + 4 * ((steps - 1) * (L + 1) + L);
+        t1 = std::max(t1, (long long)e[3]);
+        pro += (double)(p[1] - p[0]);
+        blk += (double)(e[3] - p[0]);
+        ++xcc[p[EF_PHASE_STRIDE - 1] & 7];
+        for (int st = 0; st < steps; ++st) {
+            const unsigned long long* q0 = p + 1 + 4 * (st * (L + 1));
+            l0 += (double)(q0[3] - q0[0]);
+            for (int l = 1; l < L; ++l) {
+                const unsigned long long* q = q0 + 4 * l;
+                stg[l] += (double)(q[1] - q[0]);
+                kl[l] += (double)(q[2] - q[1]);
+                ep[l] += (double)(q[3] - q[2]);
+            }
+            const unsigned long long* qh = q0 + 4 * L;
+            head += (double)(qh[3] - qh[0]);
+        }
+    }
+    if (n == 0) return;
+    const double us = 0.01 / (double)n, per = us / (double)steps;
+    std::fprintf(stderr, "phase probe (split Euler flow, last launch): %lld blocks, %d steps, span %.1f us, block %.1f us, "
+                 "start spread %.2f us, prologue %.2f us; blocks per XCC %d %d %d %d %d %d %d %d\n",
+                 n, steps, (double)(t1 - t0) * 0.01, blk * us, (double)(tl - t0) * 0.01, pro * us, xcc[0], xcc[1],
+                 xcc[2], xcc[3], xcc[4], xcc[5], xcc[6], xcc[7]);
+    std::fprintf(stderr, "  layer 0 per step (redundant, no hand-off): %.3f\n", l0 * per);
+    for (int l = 1; l < L; ++l)
+        std::fprintf(stderr, "  layer %d per step: stage (wait + copy) %.3f | k-loop %.3f | epilogue + publish %.3f\n", l,
+                     stg[l] * per, kl[l] * per, ep[l] * per);
+    std::fprintf(stderr, "  head per step (wait for the 8 partials + update): %.3f\n", head * per);
+}
+
 void flip_params(fqlpop* h);
 
 // Enqueue one population update (train) or one total_loss pass (!train).
@@ -1132,7 +1188,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     const int B = h->B, D = h->D, A = h->A, H = h->H, E = h->E, L = h->L, S = h->S;
     const int Kc = D + A, Kb = D + A + 1;
     const int B2 = 2 * B, B3 = 3 * B;
-    hipStream_t sM = h->sM, sF = h->sF, sB = h->sB;
+    hipStream_t sM = h->sM, sF = h->sF, sB = h->sB, sX = h->sX;
     h->ev_next = 0;
     h->probe_idx = 0;
     h->cr_in = h->cr_in_buf[h->cur];
@@ -1281,12 +1337,21 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     }
     const NetLayout& NC = h->critic;
     const long long sy2 = (long long)H * B2, sy1 = (long long)H * B;
-    // ---- sM: target critic on [s', a'] (params from the target arena) -----
+    // Small populations (the Euler flow runs split: DESIGN.md section 4, small-population
+    // schedule): the target critic and, later, the critic's TD-column backward run on a 4th
+    // stream sX beside the main chain, which then carries the critic forward, the Q-loss
+    // columns' backward (dQ/da) and the actor chain only.  sX forks from sM and joins sM / sB;
+    // it never waits on sB or sF (capture rule above).
+    const bool small = h->opt.small_sched && h->sX != h->sM && h->stream_fwd && h->stream_bwd && h->fused_adam &&
+                       euler_split(h, c.nz) > 1;
+    hipStream_t sT = small ? h->sX : sM;
+    dep(sM, sT);  // a' is in the target-critic input
+    // ---- sM (sX): target critic on [s', a'] (params from the target arena) -----
     if (h->stream_fwd) {
         HeadArgs ht{};
         ht.B = B; ht.D = D; ht.steps_f = (float)S;
         ht.o0 = tref(h->qt, (long long)E * B, B); ht.ld0 = B;
-        stream_fwd(c, sM, NC, h->target, h->PT, tref(h->tg_in, (long long)Kc * B), B, B, nullptr, nullptr, nullptr,
+        stream_fwd(c, sT, NC, h->target, h->PT, tref(h->tg_in, (long long)Kc * B), B, B, nullptr, nullptr, nullptr,
                    nullptr, 0, 0, 0, 0, 0, 0, HEAD_STORE, ht);
     } else {
         const NetLayout& N = NC;
@@ -1338,6 +1403,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             launch_head_fwd(HEAD_STORE, hc, sM);
         }
     }
+    dep(sT, sM);  // Q_target
     launch_loss_critic(la, sM);
     // the fused optimiser: the critic's dW + Adam is captured after the actor's dX chain, on
     // sB (idle by then), so that it runs beside that chain instead of ahead of it on a shared
@@ -1351,7 +1417,19 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
         ig.da = tref(h->da, (long long)E * A * B);
         ig.H = H; ig.D = D; ig.A = A; ig.E = E; ig.ld = B2; ig.off = B; ig.M = B;
         ig.nz = c.nz; ig.slots = h->slots;
-        if (h->stream_bwd) {
+        if (small) {
+            // the Q-loss columns [B, 2B) on sM (dQ/da: the actor chain waits for it), the TD columns
+            // [0, B) (parameter grads) on sX; the same per-column arithmetic as one launch
+            dep(sM, sX);
+            InGradArgs ig0 = ig;
+            ig0.off = 0;  // (relative to the launch's columns)
+            stream_bwd_net(c, sM, NC, tref(h->dq + B, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0),
+                           B2, B, B, 0, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, B2, h->part_cr, sM,
+                           &ig0, nullptr);
+            stream_bwd_net(c, sX, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0),
+                           B2, 0, B, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, B2, h->part_cr, sB,
+                           nullptr, &critic_dw);
+        } else if (h->stream_bwd) {
             stream_bwd_net(c, sM, NC, tref(h->dq, (long long)E * B2, B2), B2, tref(h->cr_in, (long long)Kc * B2, 0),
                            B2, 0, B2, B, h->cr_u, h->cr_h, sy2, &h->cr_mu, &h->cr_rs, B2, h->cr_du, B2, h->part_cr,
                            h->fused_adam ? sB : sM, &ig, h->fused_adam ? &critic_dw : nullptr);
@@ -1377,6 +1455,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
             // (the critical chain) is dispatched first: a dW launch dispatched ahead of it
             // takes every CU's LDS (3 blocks of 51 KB) and starves it
             dep(sM, sB);
+            if (small) dep(sX, sB);  // (and for the TD-column backward on sX)
             // actor dX chain, then the critic's grads + Adam (sB) beside the actor's (sM), then
             // the join
             std::function<void()> os_dw;
@@ -1636,14 +1715,19 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
 
         h->opt = g_engine_opts;
         const EngineOptions& eo = h->opt;
-        // three streams; serial (profiling option): every kernel of the
-        // step on sM, so a kernel trace shows uncontended durations
+        // three or four streams; serial (profiling option): every kernel
+        // of the step on sM, so a kernel trace shows uncontended durations.  With fewer than 4
+        // hardware queues the step is captured on one stream too: the HIP runtime's graph launch
+        // hands a graph's parallel branches to a pool of streams and can index past that pool
+        // when more than one of them shares the launch stream's hardware queue (a crash inside
+        // hipGraphLaunch)
         HIPCHK(hipStreamCreateWithFlags(&h->sM, hipStreamNonBlocking));
-        if (eo.serial) {
-            h->sF = h->sB = h->sM;
+        if (eo.serial || eo.hw_queues < 4) {
+            h->sF = h->sB = h->sX = h->sM;
         } else {
             HIPCHK(hipStreamCreateWithFlags(&h->sF, hipStreamNonBlocking));
             HIPCHK(hipStreamCreateWithFlags(&h->sB, hipStreamNonBlocking));
+            HIPCHK(hipStreamCreateWithFlags(&h->sX, hipStreamNonBlocking));
         }
         h->ev_pool.resize(64);
         h->euler_fused = euler_flow_supported(H, L, D, A, B) && !h->bc.ln && eo.euler_fused;
@@ -1671,7 +1755,7 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
             std::memset(h->phase_host, 0, phb);
             HIPCHK(hipHostGetDevicePointer((void**)&h->phase_dev, h->phase_host, 0));
             if (h->euler_fused && cfg->flow_steps <= 11) {
-                h->ephase_blocks = (long long)(cfg->batch_size / 16) * n_members;
+                h->ephase_blocks = (long long)(cfg->batch_size / 16) * n_members * 8;  // (split: up to 8 per tile)
                 const size_t eb = sizeof(unsigned long long) * EF_PHASE_STRIDE * h->ephase_blocks;
                 HIPCHK(hipHostMalloc((void**)&h->ephase_host, eb, hipHostMallocMapped | hipHostMallocCoherent));
                 std::memset(h->ephase_host, 0, eb);
@@ -1750,7 +1834,8 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         h->split_ok = h->stream_fwd && eo.split != 0;
         if (h->split_ok) {
             const long long tiles_per_member[SITE_N] = {B2 / 16, B / 16, B3 / 16, (long long)E * B / 16,
-                                                        (long long)E * B2 / 16, (long long)E * B2 / 16, B / 16};
+                                                        (long long)E * B2 / 16, (long long)E * B2 / 16, B / 16,
+                                                        (long long)E * B / 16};
             for (int si = 0; si < SITE_N; ++si) {
                 auto& st = h->split_site[si];
                 st.clusters = std::min(kSplitMaxClusters, tiles_per_member[si] * n);
@@ -1840,9 +1925,13 @@ int fqlpop_destroy(fqlpop_t* h) {
             (void)hipHostFree(h->phase_host);
         }
         if (h->ephase_host) {
-            euler_phase_report(h->ephase_host, h->ephase_blocks, h->L, h->S - 1);
+            if (euler_split(h, h->nz) > 1)
+                split_euler_phase_report(h->ephase_host, h->ephase_blocks, h->L, h->S - 1);
+            else
+                euler_phase_report(h->ephase_host, h->ephase_blocks, h->L, h->S - 1);
             (void)hipHostFree(h->ephase_host);
         }
+        if (h->sX && h->sX != h->sM) (void)hipStreamDestroy(h->sX);
         if (h->sF && h->sF != h->sM) (void)hipStreamDestroy(h->sF);
         if (h->sB && h->sB != h->sM) (void)hipStreamDestroy(h->sB);
         if (h->sM) (void)hipStreamDestroy(h->sM);
@@ -2153,6 +2242,7 @@ int fqlpop_sync(fqlpop_t* h) {
         HIPCHK(hipStreamSynchronize(h->sM));
         HIPCHK(hipStreamSynchronize(h->sF));
         HIPCHK(hipStreamSynchronize(h->sB));
+        HIPCHK(hipStreamSynchronize(h->sX));
         check_split_error(h);
     });
 }

@@ -17,12 +17,16 @@ from fqlpop import Population, PopulationConfig, set_engine_option  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 60
 wl = bench.WORKLOADS[sys.argv[2] if len(sys.argv) > 2 else "cube"]
-for kv in sys.argv[3:]:  # e.g. serial=1: one stream, each launch uncontended
+members = 16
+for kv in sys.argv[3:]:  # e.g. serial=1: one stream, each launch uncontended; members=2: population size
     k, v = kv.split("=")
-    set_engine_option(k, int(v))
+    if k == "members":
+        members = int(v)
+    else:
+        set_engine_option(k, int(v))
 rows = 200_000
 data = bench.synthetic_dataset(rows, wl["obs_dim"], wl["action_dim"])
-alphas, seeds = bench.population_values(16)
+alphas, seeds = bench.population_values(members)
 pop = Population(PopulationConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"],
                                   batch_size=wl["batch_size"]), alphas, seeds)
 pop.set_dataset({k: torch.as_tensor(v).cuda() for k, v in data.items()})

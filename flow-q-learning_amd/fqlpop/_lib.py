@@ -186,6 +186,17 @@ def reset_engine_options() -> None:
     check(load_library().fqlpop_reset_engine_options())
 
 
+def hw_queues_from_env() -> int | None:
+    """GPU_MAX_HW_QUEUES, the HIP runtime's hardware queues per process, if the caller set
+    it (None otherwise): Population passes it to the engine (option hw_queues), which
+    captures the step on one stream below 4."""
+    v = os.environ.get("GPU_MAX_HW_QUEUES")
+    try:
+        return max(1, min(1024, int(v))) if v else None
+    except ValueError:
+        return None
+
+
 def is_diagnostic_build() -> bool:
     return bool(load_library().fqlpop_diagnostic_build())
 

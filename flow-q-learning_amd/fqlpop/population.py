@@ -94,6 +94,9 @@ class Population:
         self.alphas = alphas.copy()
         self.seeds = seeds.copy()
         self._c = cfg.to_c()
+        hwq = _lib.hw_queues_from_env()
+        if hwq is not None:
+            _lib.set_engine_option("hw_queues", hwq)
         h = ctypes.c_void_p()
         check(self.lib.fqlpop_create(ctypes.byref(self._c), self.n, fptr(alphas),
                                      seeds.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),

@@ -81,7 +81,13 @@ const char* fqlpop_last_error(void);
  *   dw_tile_critic / dw_tile_actor (0..10), adam_nt (0..3),
  *   split (0 off, 1 auto, 2 / 4 / 8: small populations run the streamed forwards, the
  *   Euler flow and the critic / one-step backwards as clusters of 2-8 blocks per 16-column
- *   tile; bit-identical to the unsplit kernels).
+ *   tile; bit-identical to the unsplit kernels),
+ *   small_sched (0/1: with the Euler flow split, the target critic and the critic's
+ *   TD-column backward run on a fourth stream),
+ *   hw_queues (1..1024, default 4): the GPU_MAX_HW_QUEUES the caller runs the HIP runtime
+ *   with.  Below 4 the step is captured on one stream: ROCm 7's graph launch can index past
+ *   its pool of branch streams when more than one shares the launch stream's hardware queue.
+ *   A caller that sets GPU_MAX_HW_QUEUES passes it here (the Python Population does).
  * The defaults are the measured-fastest configuration.  Unknown names or values
  * out of range: FQLPOP_E_ARG.  (Round 3's schedule experiments that measured slower --
  * streams, prio, cdw_sb, dw_stagger, xstep, bc_late, fuse_dq, early_join -- were

@@ -77,3 +77,24 @@ def test_split_option_values():
         with pytest.raises(fqlpop.FqlpopError):
             fqlpop.set_engine_option("split", v)
     fqlpop.reset_engine_options()
+
+
+def test_hw_queues_option_and_env_parse(monkeypatch):
+    """hw_queues (the caller's GPU_MAX_HW_QUEUES): a validated engine option, and the value
+    the Python layer reads from the environment (below 4 the step is captured on one stream)."""
+    import pytest
+    import fqlpop
+    from fqlpop import _lib
+    assert fqlpop.get_engine_option("hw_queues") == 4
+    fqlpop.set_engine_option("hw_queues", 2)
+    assert fqlpop.get_engine_option("hw_queues") == 2
+    fqlpop.reset_engine_options()
+    assert fqlpop.get_engine_option("hw_queues") == 4
+    with pytest.raises(fqlpop.FqlpopError):
+        fqlpop.set_engine_option("hw_queues", 0)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "2")
+    assert _lib.hw_queues_from_env() == 2
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "junk")
+    assert _lib.hw_queues_from_env() is None
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES")
+    assert _lib.hw_queues_from_env() is None

@@ -64,6 +64,16 @@ def test_split_bit_identical_to_unsplit_cube(n, F):
     _same(got, ref)
 
 
+@pytest.mark.parametrize("n", [1, 2])
+def test_small_population_schedule_bit_identical(n):
+    """The small-population schedule (engine option small_sched: the target critic and the
+    critic's TD-column backward on a fourth stream, the Q-loss columns' backward as a launch
+    of its own) changes where launches run, not what they compute."""
+    ref = _run({"split": 8, "small_sched": 0}, n)
+    got = _run({"split": 8, "small_sched": 1}, n)
+    _same(got, ref)
+
+
 def test_split_auto_bit_identical_antsoccer_shape():
     """BASELINE C3 shapes (obs 42, act 8, B = 1024), one member: auto splits the Euler
     flow (64 tiles x 4 blocks), the BC forward and the target critic (128 tiles x 2); the
