@@ -1684,7 +1684,10 @@ DEV int sp_fidx(int k, int col) { return ((((k >> 4) << 6) + ((k & 3) << 4) + co
 DEV void sp_fail(const SplitSync& sy) {
     __hip_atomic_store((gu32_t*)sy.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// block start: the ticket (cluster * F + slice) and the launch generation, block-uniform
+// block start: the ticket (cluster * F + slice) and the launch generation, block-uniform.
+// readfirstlane: values read from LDS are not known to be uniform, and everything derived
+// from the ticket (slot, parameter base, buffer resources) would sit in VGPRs, every buffer
+// load then in a waterfall loop (round 4: the split k-loops ran 4x their MFMA time)
 DEV int sp_begin(const SplitSync& sy, int clusters, unsigned* bc) {
     if (threadIdx.x == 0) {
         bc[0] = __hip_atomic_fetch_add((gu32_t*)(sy.cnt + (long long)clusters * SP_CNT_STRIDE), 1u, __ATOMIC_RELAXED,
@@ -1692,7 +1695,7 @@ DEV int sp_begin(const SplitSync& sy, int clusters, unsigned* bc) {
         bc[1] = __hip_atomic_load((const gu32_t*)sy.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    return (int)bc[0];
+    return __builtin_amdgcn_readfirstlane((int)bc[0]);
 }
 // block end (every block, every path): the last one to exit advances the site's generation and
 // zeroes the launch's counters (every other block has taken its ticket, made its last-arriver
@@ -1703,7 +1706,7 @@ DEV void sp_end(const SplitSync& sy, int clusters, int blocks, unsigned* bc) {
         bc[0] = __hip_atomic_fetch_add((gu32_t*)(sy.cnt + (long long)(clusters + 1) * SP_CNT_STRIDE), 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if (bc[0] == (unsigned)blocks - 1) {
+    if (__builtin_amdgcn_readfirstlane(bc[0]) == (unsigned)blocks - 1) {
         for (int c = threadIdx.x; c < clusters + 2; c += blockDim.x)
             __hip_atomic_store((gu32_t*)(sy.cnt + (long long)c * SP_CNT_STRIDE), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32_t*)sy.gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1764,7 +1767,7 @@ DEV bool sp_last(const SplitSync& sy, int cl, int F, unsigned* bc) {
         bc[0] = __hip_atomic_fetch_add((gu32_t*)(sy.cnt + (long long)cl * SP_CNT_STRIDE), 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    return bc[0] == (unsigned)F - 1;
+    return __builtin_amdgcn_readfirstlane(bc[0]) == (unsigned)F - 1;
 }
 
 // A fragments of TPW consecutive features: W[k][col .. col + TPW - 1] (components 0..TPW-1)
@@ -1847,11 +1850,11 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
 
     const int tiles = g.M / NC, clusters = tiles * g.ny * g.nz;
     const int ticket = sp_begin(a.sync, clusters, bc);
-    const unsigned gen = bc[1];
+    const unsigned gen = __builtin_amdgcn_readfirstlane(bc[1]);
     const int cl = ticket / F, f = ticket % F, fb = f * FB;
-    const int tl = cl % tiles, yz = cl / tiles;
-    const int y = yz % g.ny, z = yz / g.ny;
-    const int slot = g.slots[z];
+    const int tl = __builtin_amdgcn_readfirstlane(cl % tiles), yz = cl / tiles;
+    const int y = __builtin_amdgcn_readfirstlane(yz % g.ny), z = __builtin_amdgcn_readfirstlane(yz / g.ny);
+    const int slot = __builtin_amdgcn_readfirstlane(g.slots[z]);
     const int c0 = tl * NC;
     const int tid = threadIdx.x, lane = tid & 63;
     const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2038,8 +2041,10 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
             stamp(pst, 0, 3);
         }
         // ---- hidden layers 1 .. L-1, split ----
-        // (the Euler flow at TPW = 2 keeps the 8-deep ring: a deeper one spills)
-        constexpr int RPF = EULER && TPW == 2 ? 8 : sp_pf<TPW>();
+        // ring depth per form, the deepest that does not spill (256 VGPRs at 2 waves per SIMD):
+        // a k-step's loads wait ~1 us under load, its MFMAs take TPW x 32-40 cycles
+        constexpr int RPF = EULER ? (TPW == 1 ? 32 : 8)
+                                  : (TPW == 4 ? (LN ? 8 : 16) : TPW == 2 ? 32 : 64);
         float4 ring[RPF];
         const int col = fb + 16 * TPW * q + TPW * li;
         const int lo = lk * H + col;
@@ -2868,11 +2873,11 @@ __global__ __launch_bounds__(SP_NT, 2) void split_bwd_kernel(const StreamBwdArgs
 
     const int tiles = g.M / NC, clusters = tiles * g.ny * g.nz;
     const int ticket = sp_begin(sync, clusters, bc);
-    const unsigned gen = bc[1];
+    const unsigned gen = __builtin_amdgcn_readfirstlane(bc[1]);
     const int cl = ticket / F, f = ticket % F, fb = f * FB;
-    const int tl = cl % tiles, yz = cl / tiles;
-    const int y = yz % g.ny, z = yz / g.ny;
-    const int slot = g.slots[z];
+    const int tl = __builtin_amdgcn_readfirstlane(cl % tiles), yz = cl / tiles;
+    const int y = __builtin_amdgcn_readfirstlane(yz % g.ny), z = __builtin_amdgcn_readfirstlane(yz / g.ny);
+    const int slot = __builtin_amdgcn_readfirstlane(g.slots[z]);
     const int c0 = tl * NC;
     const int tid = threadIdx.x, lane = tid & 63;
     const int q = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -79,6 +79,7 @@ struct EngineOptions {
                            // 16-column tile (bit-identical); 0 off, 1 auto, 2 / 4 / 8 blocks where they fit
     int small_sched = 1;   // small populations (the Euler flow split): target critic and the critic's
                            // TD-column backward on a 4th stream beside the main chain (bit-identical)
+    int split_blocks = 256;  // the most blocks of a split forward / Euler launch (F shrinks to fit)
     int hw_queues = 4;     // the HIP runtime's hardware queues per process (GPU_MAX_HW_QUEUES, which the
                            // caller sets; the Python layer passes it): below 4 the step is captured on
                            // one stream (graph launch and hardware queues)
@@ -105,6 +106,7 @@ const EngineOptionRef kEngineOptions[] = {
     {"split", &EngineOptions::split, 0, 8},
     {"small_sched", &EngineOptions::small_sched, 0, 1},
     {"hw_queues", &EngineOptions::hw_queues, 1, 1024},
+    {"split_blocks", &EngineOptions::split_blocks, 64, 1024},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -969,7 +971,7 @@ void stream_fwd(const Ctx& c, hipStream_t s, const NetLayout& N, const float* ar
     if (sk & bit) return;
     const int site = &N == &h->bc ? SITE_BCF : &N == &h->os ? SITE_OSF : arena == h->target ? SITE_TGT : SITE_CRF;
     const long long clusters = (long long)(M / 16) * N.E * c.nz;
-    const int F = split_fwd_supported(N.H, N.L, N.in_dim, N.out_dim, M) ? split_factor(h, clusters, false) : 1;
+    const int F = split_fwd_supported(N.H, N.L, N.in_dim, N.out_dim, M) ? split_factor(h, clusters, false, h->opt.split_blocks) : 1;
     if (F > 1) {
         SplitFwdArgs sa{};
         sa.s = a;
@@ -984,7 +986,7 @@ void stream_fwd(const Ctx& c, hipStream_t s, const NetLayout& N, const float* ar
 int euler_split(const fqlpop* h, int nz) {
     const NetLayout& N = h->bc;
     if (!h->euler_fused || !split_fwd_supported(N.H, N.L, N.in_dim, N.out_dim, h->B)) return 1;
-    return split_factor(h, (long long)(h->B / 16) * nz, true);
+    return split_factor(h, (long long)(h->B / 16) * nz, true, h->opt.split_blocks);
 }
 SplitFwdArgs euler_split_args(fqlpop* h, const EulerArgs& ea, hipStream_t s) {
     const NetLayout& N = h->bc;
@@ -1002,12 +1004,15 @@ SplitFwdArgs euler_split_args(fqlpop* h, const EulerArgs& ea, hipStream_t s) {
     sa.sync = split_prep(h, SITE_EULER, (long long)(ea.B / 16) * ea.nz, s);
     return sa;
 }
+long long euler_blocks(const fqlpop* h, int nz) { return (long long)(h->B / 16) * nz * euler_split(h, nz); }
 void launch_euler(fqlpop* h, const EulerArgs& ea, hipStream_t s) {
     const int F = euler_split(h, ea.nz);
+    // every block of the launch writes its two probe stamps and its phase stamps
+    ARGCHK(ea.probe == nullptr || euler_blocks(h, ea.nz) <= h->probe_blocks, "Euler probe: too many blocks");
+    ARGCHK(ea.phase == nullptr || euler_blocks(h, ea.nz) <= h->ephase_blocks, "Euler phase probe: too many blocks");
     if (F > 1) launch_split_fwd(HEAD_EULER, false, true, F, euler_split_args(h, ea, s), s);
     else launch_euler_flow(ea, s);
 }
-long long euler_blocks(const fqlpop* h, int nz) { return (long long)(h->B / 16) * nz * euler_split(h, nz); }
 
 // FQLPOP_SKIP (diagnostic builds only; TIMING EXPERIMENT, results are garbage): bit mask
 // of launches left out of the step, to measure each one's marginal cost in the concurrent
@@ -1737,7 +1742,8 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         h->fused_adam = h->stream_bwd && H % 128 == 0 && L <= GEMM_GROUP_MAX && h->critic.off == 0 && eo.fused_adam;
         if (h->euler_fused) {  // dominant kernel: one persistent Euler launch per step
             h->probe_pairs = 1;
-            h->probe_blocks = std::max<long long>((long long)(cfg->batch_size / 16) * n_members, kSplitMaxBlocks);
+            // (the split Euler launch: up to 8 blocks per 16-column tile)
+            h->probe_blocks = std::max<long long>((long long)(cfg->batch_size / 16) * n_members * 8, kSplitMaxBlocks);
         } else {               // dominant kernel: the Euler hidden-layer GEMMs
             h->probe_pairs = std::max(1, (cfg->flow_steps - 1) * (cfg->num_hidden - 1));
             h->probe_blocks = (long long)((cfg->hidden_dim + 63) / 64) * ((cfg->batch_size + 63) / 64) * n_members;
