@@ -98,3 +98,20 @@ def test_hw_queues_option_and_env_parse(monkeypatch):
     assert _lib.hw_queues_from_env() is None
     monkeypatch.delenv("GPU_MAX_HW_QUEUES")
     assert _lib.hw_queues_from_env() is None
+
+
+def test_population_passes_hw_queues_before_create(monkeypatch):
+    """Population hands GPU_MAX_HW_QUEUES to the engine before fqlpop_create (here create
+    then fails: no GPU in the CPU suite), so a caller running the HIP runtime with 2 queues
+    gets the one-stream capture instead of the runtime's crash in hipGraphLaunch."""
+    import fqlpop
+    from fqlpop import Population, PopulationConfig
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "2")
+    try:
+        try:
+            Population(PopulationConfig(), [3.0], [1]).close()  # (a GPU host: create succeeds)
+        except fqlpop.FqlpopError:
+            pass
+        assert fqlpop.get_engine_option("hw_queues") == 2
+    finally:
+        fqlpop.reset_engine_options()
