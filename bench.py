@@ -149,33 +149,109 @@ def gpu_clock_power(device_index: int) -> dict:
     return out
 
 
-def cpu_baseline(wl: dict, data: dict, budget_s: float) -> dict:
-    """The oracle's float32 PyTorch-CPU restatement (kind "port") of one member's
-    update on the same synthetic data, timed on this host's cores: at as many torch threads
-    as the CPUs this process may run on (sched_getaffinity) and at 16 (the box's
-    OMP_NUM_THREADS), half the budget each; the faster is the value, both are recorded."""
+CPU_LEG_CAP_S = 20.0  # the whole CPU leg, warm-up updates included (the driver's run must finish)
+
+
+def _cgroup_cpu_quota():
+    """CPUs granted by the cgroup CPU quota (cgroup v2 cpu.max, else v1 cfs_quota / period),
+    rounded up; None when no quota is set or the files are unreadable."""
+    def rd(p):
+        try:
+            with open(p) as f:
+                return f.read().split()
+        except OSError:
+            return None
+
+    v2 = rd("/sys/fs/cgroup/cpu.max")
+    if v2 and len(v2) >= 2 and v2[0] != "max":
+        try:
+            return max(1, -(-int(v2[0]) // int(v2[1])))
+        except ValueError:
+            return None
+    q, p = rd("/sys/fs/cgroup/cpu/cpu.cfs_quota_us"), rd("/sys/fs/cgroup/cpu/cpu.cfs_period_us")
+    if q and p:
+        try:
+            qi, pi = int(q[0]), int(p[0])
+        except ValueError:
+            return None
+        if qi > 0 and pi > 0:
+            return max(1, -(-qi // pi))
+    return None
+
+
+def cpu_allotment() -> dict:
+    """The CPUs this process may actually keep busy: the smallest of sched_getaffinity, the
+    cgroup quota and OMP_NUM_THREADS (the box exports the job's CPU share there; its
+    affinity mask and os.cpu_count() show the whole 256-CPU host)."""
     host = host_cpu()
-    counts = sorted({max(1, host["affinity_cpus"] or os.cpu_count() or 1), 16})
-    runs = {}
-    for threads in counts:
-        runs[threads] = _cpu_rate(wl, data, budget_s / len(counts), threads)
-    best = max(runs, key=lambda t: runs[t][0])
-    rate, steps, el = runs[best]
+    quota = _cgroup_cpu_quota()
+    omp = host["omp_num_threads"]
+    try:
+        omp = int(omp) if omp else None
+    except ValueError:
+        omp = None
+    cands = [c for c in (host["affinity_cpus"], quota, omp) if c]
+    host["cgroup_quota_cpus"] = quota
+    host["effective_cpus"] = max(1, min(cands) if cands else (os.cpu_count() or 1))
+    return host
+
+
+def cpu_baseline(wl: dict, data: dict, budget_s: float, thread_counts=None) -> dict:
+    """The oracle's float32 PyTorch-CPU restatement (kind "port") of one member's
+    update on the same synthetic data, timed on this host's cores at the effective CPU
+    allotment (cpu_allotment) and at 1 thread.  Hard wall budget: min(budget_s,
+    CPU_LEG_CAP_S) for the whole leg, split over the thread counts; each count's warm-up
+    update counts against its share, the timing loop stops at the share's deadline (so a
+    count overruns it by at most one update), and a count whose warm-up update alone
+    exceeds its share is abandoned and recorded as such.  The best completed count is the
+    value.  ``thread_counts`` overrides the counts (tests)."""
+    host = cpu_allotment()
+    eff = host["effective_cpus"]
+    counts = list(thread_counts) if thread_counts else ([eff, 1] if eff > 1 else [1])
+    total = min(float(budget_s), CPU_LEG_CAP_S)
+    share = total / len(counts)
+    prev_threads = torch.get_num_threads()
+    runs, abandoned = {}, {}
+    t_leg = time.perf_counter()
+    try:
+        for threads in counts:
+            r = _cpu_rate(wl, data, share, threads)
+            if r["steps"] > 0:
+                runs[threads] = r
+            else:
+                abandoned[str(threads)] = r["note"]
+    finally:
+        torch.set_num_threads(prev_threads)
+    leg_s = time.perf_counter() - t_leg
     B = wl["batch_size"]
-    return {"value": rate, "unit": "member-grad-steps/s", "cores": best, "kind": "port", "host": host,
-            "rates_by_threads": {str(t): round(r[0], 3) for t, r in runs.items()},
-            "sample": f"{steps} sequential update() steps of 1 member (alpha=10, B={B}, H=512) in {el:.1f} s, "
-                      f"float32 PyTorch-CPU restatement (oracle/fql_torch.py), torch threads={best}: the faster of "
-                      f"{' and '.join(str(t) for t in counts)} threads (sched_getaffinity allows "
-                      f"{host['affinity_cpus']} CPUs, OMP_NUM_THREADS {host['omp_num_threads']}, os.cpu_count() "
+    if not runs:
+        return {"value": None, "unit": "member-grad-steps/s", "cores": None, "kind": "port", "host": host,
+                "rates_by_threads": {}, "abandoned": abandoned, "leg_s": round(leg_s, 2),
+                "sample": f"no thread count finished an update within its {share:.1f} s share"}
+    best = max(runs, key=lambda t: runs[t]["rate"])
+    r = runs[best]
+    return {"value": r["rate"], "unit": "member-grad-steps/s", "cores": best, "kind": "port", "host": host,
+            "rates_by_threads": {str(t): round(x["rate"], 3) for t, x in runs.items()},
+            "abandoned": abandoned, "leg_s": round(leg_s, 2), "budget_s": round(total, 2),
+            "longest_update_s": round(max(x["longest_update_s"] for x in runs.values()), 3),
+            "sample": f"{r['steps']} sequential update() steps of 1 member (alpha=10, B={B}, H=512) in "
+                      f"{r['elapsed']:.1f} s after a {r['warmup_s']:.2f} s warm-up update, float32 PyTorch-CPU "
+                      f"restatement (oracle/fql_torch.py), torch threads={best}: the best of "
+                      f"{', '.join(str(t) for t in counts)} thread(s), {share:.1f} s wall budget each "
+                      f"(effective CPUs {eff} = min of sched_getaffinity {host['affinity_cpus']}, cgroup quota "
+                      f"{host['cgroup_quota_cpus']}, OMP_NUM_THREADS {host['omp_num_threads']}; os.cpu_count() "
                       f"{host['os_cpu_count']}). BASELINE C1 (1k steps) extrapolated from this rate: "
-                      f"{1000.0 / rate:.0f} s"}
+                      f"{1000.0 / r['rate']:.0f} s"}
 
 
-def _cpu_rate(wl: dict, data: dict, budget_s: float, threads: int):
+def _cpu_rate(wl: dict, data: dict, budget_s: float, threads: int) -> dict:
+    """Updates of one member at ``threads`` torch threads until ``budget_s`` of wall time
+    (warm-up included) is spent.  steps == 0 means the warm-up update alone used the budget."""
     from oracle import fql_oracle as O
     from oracle.fql_torch import TorchFQL
 
+    t_start = time.perf_counter()
+    deadline = t_start + budget_s
     torch.set_num_threads(threads)
     cfg = O.OracleConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"], batch_size=wl["batch_size"],
                          alpha=10.0)
@@ -190,15 +266,25 @@ def _cpu_rate(wl: dict, data: dict, budget_s: float, threads: int):
               "z_d": torch.randn(B, A), "z_metric": torch.randn(B, A)}
         return b, nz
 
+    t_w = time.perf_counter()
     agent.update(*draw())  # warm-up
-    steps, t0 = 0, time.perf_counter()
+    warm = time.perf_counter() - t_w
+    t0 = time.perf_counter()
+    if t0 >= deadline:
+        return {"rate": 0.0, "steps": 0, "elapsed": 0.0, "warmup_s": warm, "longest_update_s": warm,
+                "note": f"abandoned: setup + warm-up update took {t0 - t_start:.2f} s > {budget_s:.2f} s share"}
+    steps, el, longest = 0, 0.0, warm
     while True:
+        t_u = time.perf_counter()
         agent.update(*draw())
         steps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s and steps >= 3:
+        now = time.perf_counter()
+        longest = max(longest, now - t_u)
+        el = now - t0
+        if now >= deadline:
             break
-    return steps / el, steps, el
+    return {"rate": steps / el, "steps": steps, "elapsed": el, "warmup_s": warm, "longest_update_s": longest,
+            "note": None}
 
 
 def eval_rollout_leg(pop, wl: dict, n_envs: int, steps: int, dev) -> dict:

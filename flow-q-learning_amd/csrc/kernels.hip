@@ -1682,7 +1682,7 @@ typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 DEV int sp_fidx(int k, int col) { return ((((k >> 4) << 6) + ((k & 3) << 4) + col) << 2) + ((k >> 2) & 3); }
 
 DEV void sp_fail(const SplitSync& sy) {
-    __hip_atomic_store((gu32_t*)sy.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32_t*)sy.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // host-mapped word
 }
 // block start: the ticket (cluster * F + slice) and the launch generation, block-uniform.
 // readfirstlane: values read from LDS are not known to be uniform, and everything derived

@@ -91,6 +91,16 @@ struct EngineOptions {
 // main chain's early joins.)
 EngineOptions g_engine_opts;
 
+// Streams (= parallel branches of the step's graph) the step is captured on.  The HIP
+// runtime's graph launch is only safe for branches <= hardware queues (DESIGN.md section 4,
+// graph launch and hardware queues), so below kStepBranches queues the step runs on one
+// stream.  Any schedule change that adds a stream raises kStepBranches and, through the
+// check in graph_for, can never be captured beside fewer queues than it has branches.
+constexpr int kStepBranches = 4;  // sM, sF, sB, sX
+int step_streams(const EngineOptions& eo) {
+    return (eo.serial || eo.hw_queues < kStepBranches) ? 1 : kStepBranches;
+}
+
 struct EngineOptionRef {
     const char* name;
     int EngineOptions::*field;
@@ -267,7 +277,8 @@ struct fqlpop {
         unsigned* gen = nullptr;
         long long clusters = 0;    // capacity
     } split_site[8];
-    unsigned* split_err = nullptr;
+    unsigned* split_err = nullptr;       // device pointer of split_err_host (mapped, coherent host memory)
+    unsigned* split_err_host = nullptr;  // the host reads it without a copy or a synchronisation
     bool split_ok = false;
     bool stream_fwd = false;       // whole-network forward launches (stream_fwd_kernel)
     bool stream_bwd = false;       // whole-network dX chains (stream_bwd_kernel)
@@ -304,6 +315,7 @@ struct fqlpop {
     bool probe_pending[2] = {false, false};
     double probe_total_ms = 0.0;
     long long probe_launches = 0;
+    long long probe_blocks_seen = 0, probe_blocks_expected = 0;  // stamped / launched blocks (coverage)
     double clock_check_event_us = 0.0, clock_check_stamp_us = 0.0;
     std::map<long long, Graphs> graphs;  // key: mode, active count, probe set, current buffer
 
@@ -1534,6 +1546,15 @@ Graphs& graph_for(fqlpop* h, bool train, bool inj_batch, bool inj_noise, bool re
         if (gr.exec) HIPCHK(hipGraphExecDestroy(gr.exec));
         gr.exec = nullptr;
         hipGraph_t graph;
+        {   // the hardware-queue invariant: no more branches than the runtime has queues
+            std::vector<hipStream_t> ss;
+            for (hipStream_t s : {h->sM, h->sF, h->sB, h->sX})
+                if (std::find(ss.begin(), ss.end(), s) == ss.end()) ss.push_back(s);
+            if ((int)ss.size() > 1 && (int)ss.size() > h->opt.hw_queues)
+                throw FqErr{FQLPOP_E_STATE, "step graph would have " + std::to_string(ss.size()) +
+                                                " parallel branches on " + std::to_string(h->opt.hw_queues) +
+                                                " hardware queues (hipGraphLaunch is unsafe then)"};
+        }
         HIPCHK(hipStreamBeginCapture(h->sM, hipStreamCaptureModeRelaxed));
         try {
             enqueue(h, train, inj_batch, inj_noise);
@@ -1574,16 +1595,40 @@ void probe_consume(fqlpop* h, int set) {
         if (us < 0) continue;  // launch not probed
         h->probe_total_ms += us * 1e-3;
         ++h->probe_launches;
+        for (long long b = 0; b < nb; ++b) h->probe_blocks_seen += v[per * p + 2 * b] && v[per * p + 2 * b + 1];
+        h->probe_blocks_expected += nb;
     }
+    // cleared after reading, so every launch's coverage counts only its own stamps (the set's
+    // next launch is enqueued after this: fqlpop_step consumes a set before reusing it)
+    std::memset(h->probe_host + per * set * h->probe_pairs, 0, sizeof(unsigned long long) * v.size());
     h->probe_pending[set] = false;
 }
 
+void sync_all_streams(fqlpop* h) {
+    for (hipStream_t s : {h->sM, h->sF, h->sB, h->sX})
+        if (s) HIPCHK(hipStreamSynchronize(s));
+}
+
 void update_slots(fqlpop* h) {
+    const int prev = h->nz;
     h->h_slots.clear();
     for (int i = 0; i < h->n; ++i)
         if (h->active[i]) h->h_slots.push_back(i);
     h->nz = (int)h->h_slots.size();
     HIPCHK(hipStreamSynchronize(h->sM));
+    if (h->nz != prev) {
+        // a changed active count changes the cluster count of every split site: exchange words
+        // of clusters the next launches do not rewrite would keep old tags, and the 24-bit
+        // generation in a tag repeats after 2^24 launches.  Tag 0 matches no hand-off.
+        bool any = false;
+        for (auto& st : h->split_site) any |= st.xch != nullptr;
+        if (any) {
+            sync_all_streams(h);
+            for (auto& st : h->split_site)
+                if (st.xch) HIPCHK(hipMemset(st.xch, 0, split_cluster_bytes() * st.clusters));
+            HIPCHK(hipDeviceSynchronize());
+        }
+    }
     if (h->nz) HIPCHK(hipMemcpy(h->slots, h->h_slots.data(), sizeof(int) * h->nz, hipMemcpyHostToDevice));
 }
 
@@ -1602,14 +1647,15 @@ int guard(F&& f) {
     }
 }
 
-// A split launch whose hand-off wait gave up (kernels.hip, sp_wait) left invalid results:
+bool split_error_pending(const fqlpop* h) {
+    return h->split_err_host && __atomic_load_n(h->split_err_host, __ATOMIC_ACQUIRE) != 0;
+}
+
+// A split launch whose hand-off wait gave up (kernels.hip, sp_fail) left invalid results:
 // report it (once) instead of returning them.  The caller has synchronised the streams.
 void check_split_error(fqlpop* h) {
-    if (!h->split_err) return;
-    unsigned e = 0;
-    HIPCHK(hipMemcpy(&e, h->split_err, sizeof(e), hipMemcpyDeviceToHost));
-    if (e != 0) {
-        HIPCHK(hipMemset(h->split_err, 0, sizeof(e)));
+    if (split_error_pending(h)) {
+        __atomic_store_n(h->split_err_host, 0u, __ATOMIC_RELEASE);
         for (auto& st : h->split_site)  // a launch that gave up may have left its counters set
             if (st.cnt) HIPCHK(hipMemset(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (st.clusters + 2)));
         throw FqErr{FQLPOP_E_STATE, "a split launch's hand-off wait timed out (blocks of a cluster not resident "
@@ -1660,6 +1706,13 @@ int fqlpop_get_engine_option(const char* name, int* value) {
 
 int fqlpop_reset_engine_options(void) {
     return guard([&] { g_engine_opts = EngineOptions{}; });
+}
+
+int fqlpop_step_streams(int* n_streams) {
+    return guard([&] {
+        ARGCHK(n_streams != nullptr, "null argument");
+        *n_streams = step_streams(g_engine_opts);
+    });
 }
 
 int fqlpop_diagnostic_build(void) {
@@ -1727,7 +1780,7 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         // when more than one of them shares the launch stream's hardware queue (a crash inside
         // hipGraphLaunch)
         HIPCHK(hipStreamCreateWithFlags(&h->sM, hipStreamNonBlocking));
-        if (eo.serial || eo.hw_queues < 4) {
+        if (step_streams(eo) == 1) {
             h->sF = h->sB = h->sX = h->sM;
         } else {
             HIPCHK(hipStreamCreateWithFlags(&h->sF, hipStreamNonBlocking));
@@ -1852,8 +1905,11 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
                 HIPCHK(hipMalloc(&st.gen, 64));
                 HIPCHK(hipMemset(st.gen, 0, 64));
             }
-            HIPCHK(hipMalloc(&h->split_err, 64));
-            HIPCHK(hipMemset(h->split_err, 0, 64));
+            // the error word lives in host memory so that every entry point can test it without a
+            // device-to-host copy (fqlpop_step does, before it enqueues more steps)
+            HIPCHK(hipHostMalloc((void**)&h->split_err_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
+            std::memset(h->split_err_host, 0, 64);
+            HIPCHK(hipHostGetDevicePointer((void**)&h->split_err, h->split_err_host, 0));
         }
         h->cr_dh = h->alloc((long long)H * B2 * E);
         h->bc_dh = h->alloc((long long)H * B);
@@ -1909,7 +1965,7 @@ int fqlpop_destroy(fqlpop_t* h) {
             if (st.cnt) (void)hipFree(st.cnt);
             if (st.gen) (void)hipFree(st.gen);
         }
-        if (h->split_err) (void)hipFree(h->split_err);
+        if (h->split_err_host) (void)hipHostFree(h->split_err_host);
         for (hipEvent_t e : {h->ev_sample, h->ev_bcfwd, h->ev_bcloss, h->ev_flow, h->ev_bdone, h->ev_t0, h->ev_t1})
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
@@ -1991,6 +2047,10 @@ int fqlpop_step(fqlpop_t* h, int n_steps) {
     return guard([&] {
         ARGCHK(h, "null handle");
         ARGCHK(n_steps >= 0, "n_steps must be >= 0");
+        if (split_error_pending(h)) {  // a stale error stops training (no copy, no sync when clear)
+            sync_all_streams(h);
+            check_split_error(h);
+        }
         if (h->ds[0].rows == 0) throw FqErr{FQLPOP_E_STATE, "no training dataset set (fqlpop_set_dataset)"};
         HIPCHK(hipSetDevice(h->device));
         for (int i = 0; i < n_steps; ++i) {
@@ -2140,6 +2200,7 @@ static void state_copy(fqlpop* h, int member, int which, float* flat, const floa
     std::vector<float> blk((size_t)h->P), tblk((size_t)h->PT, 0.f);
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
+    check_split_error(h);  // never export (checkpoint, member copy) parameters a failed launch wrote
     HIPCHK(hipMemcpy(blk.data(), arena + (long long)member * h->P, sizeof(float) * h->P, hipMemcpyDeviceToHost));
     if (which == 0)
         HIPCHK(hipMemcpy(tblk.data(), h->target + (long long)member * h->PT, sizeof(float) * h->PT,
@@ -2194,6 +2255,7 @@ int fqlpop_get_count(fqlpop_t* h, int member, int32_t* count) {
         ARGCHK(count, "null argument");
         HIPCHK(hipSetDevice(h->device));
         HIPCHK(hipDeviceSynchronize());
+        check_split_error(h);
         HIPCHK(hipMemcpy(count, h->count + member, sizeof(int), hipMemcpyDeviceToHost));
     });
 }
@@ -2245,10 +2307,7 @@ int fqlpop_sync(fqlpop_t* h) {
     return guard([&] {
         ARGCHK(h, "null handle");
         HIPCHK(hipSetDevice(h->device));
-        HIPCHK(hipStreamSynchronize(h->sM));
-        HIPCHK(hipStreamSynchronize(h->sF));
-        HIPCHK(hipStreamSynchronize(h->sB));
-        HIPCHK(hipStreamSynchronize(h->sX));
+        sync_all_streams(h);
         check_split_error(h);
     });
 }
@@ -2332,6 +2391,18 @@ int fqlpop_set_probe(fqlpop_t* h, int enable) {
         h->probe = enable != 0;
         h->probe_total_ms = 0.0;
         h->probe_launches = 0;
+        h->probe_blocks_seen = h->probe_blocks_expected = 0;
+    });
+}
+
+int fqlpop_probe_coverage(fqlpop_t* h, int64_t* blocks_seen, int64_t* blocks_expected) {
+    return guard([&] {
+        ARGCHK(h && blocks_seen && blocks_expected, "null argument");
+        HIPCHK(hipSetDevice(h->device));
+        for (int st = 0; st < 2; ++st)
+            if (h->probe_pending[st]) probe_consume(h, st);
+        *blocks_seen = h->probe_blocks_seen;
+        *blocks_expected = h->probe_blocks_expected;
     });
 }
 

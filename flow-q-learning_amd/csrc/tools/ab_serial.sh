@@ -2,14 +2,14 @@
 # Same-box per-kernel A/B of builds on one stream (bench.py --serial): a rocprofv3 kernel trace of
 # a short bench per build, then each build's average for the kernels matching a regex.
 #   bash flow-q-learning_amd/csrc/tools/ab_serial.sh <regex> new ref ...   ("new" = the working
-#   tree's libfqlpop.so, X = fqlpop/libfqlpop_X.so through FQLPOP_LIB)
+#   tree's libfqlpop.so, X = csrc/devlib/libfqlpop_X.so through FQLPOP_LIB)
 set -uo pipefail
 RX=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 for f in "$@"; do
-  if [ "$f" = new ]; then unset FQLPOP_LIB; else export FQLPOP_LIB=$R/flow-q-learning_amd/fqlpop/libfqlpop_$f.so; fi
+  if [ "$f" = new ]; then unset FQLPOP_LIB; else export FQLPOP_LIB=$R/flow-q-learning_amd/csrc/devlib/libfqlpop_$f.so; fi
 
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/abs_$f" -o run -- \
       python3 "$R/bench.py" --diagnostic --serial --steps 60 --warmup 10 --no-cpu-baseline --kernel-iters 1 --no-probe --preheat-ms 0 \

@@ -4,7 +4,7 @@ Runs 20 device-sampled population steps of the cube headline shape (4 members, B
 H = 512) and prints a SHA-256 over every member's parameters and the last info rows.
 Run it once per build (FQLPOP_LIB selects a second library) and compare the digests:
     python flow-q-learning_amd/csrc/tools/bitcmp.py
-    FQLPOP_LIB=$PWD/flow-q-learning_amd/fqlpop/libfqlpop_ref.so python flow-q-learning_amd/csrc/tools/bitcmp.py
+    FQLPOP_LIB=$PWD/flow-q-learning_amd/csrc/devlib/libfqlpop_ref.so python flow-q-learning_amd/csrc/tools/bitcmp.py
 """
 import hashlib
 import os

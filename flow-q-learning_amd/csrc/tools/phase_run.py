@@ -1,8 +1,8 @@
 """Diagnostics: run N population steps of the bench workload and close, so that the
 FQLPOP_PHASE_PROBE reports (printed on stderr at destroy) describe in-step launches.
 
-  make -C flow-q-learning_amd/csrc PHASE=1 OUT=../fqlpop/libfqlpop_phase.so   # stamps compiled in
-  FQLPOP_LIB=$PWD/flow-q-learning_amd/fqlpop/libfqlpop_phase.so FQLPOP_PHASE_PROBE=1 \
+  make -C flow-q-learning_amd/csrc PHASE=1 OUT=devlib/libfqlpop_phase.so   # stamps compiled in
+  FQLPOP_LIB=$PWD/flow-q-learning_amd/csrc/devlib/libfqlpop_phase.so FQLPOP_PHASE_PROBE=1 \
       python flow-q-learning_amd/csrc/tools/phase_run.py [steps] [workload] [NAME=VALUE engine options ...]
 (the production build compiles the stamps out: their disabled branch cost 0.3 % in the step)
 """

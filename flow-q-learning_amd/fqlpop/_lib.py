@@ -83,6 +83,9 @@ _SIGS = {
     "fqlpop_get_engine_option": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     "fqlpop_reset_engine_options": (ctypes.c_int, []),
     "fqlpop_diagnostic_build": (ctypes.c_int, []),
+    "fqlpop_step_streams": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "fqlpop_probe_coverage": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                             ctypes.POINTER(ctypes.c_int64)]),
     "fqlpop_create": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.c_int, _F,
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_int,
                                      ctypes.POINTER(_P)]),
@@ -184,6 +187,14 @@ def get_engine_option(name: str) -> int:
 
 def reset_engine_options() -> None:
     check(load_library().fqlpop_reset_engine_options())
+
+
+def step_streams() -> int:
+    """Parallel branches (streams) a population created now would capture its step on
+    (fqlpop_step_streams; no GPU call)."""
+    v = ctypes.c_int()
+    check(load_library().fqlpop_step_streams(ctypes.byref(v)))
+    return v.value
 
 
 def hw_queues_from_env() -> int | None:

@@ -94,13 +94,20 @@ class Population:
         self.alphas = alphas.copy()
         self.seeds = seeds.copy()
         self._c = cfg.to_c()
+        # the engine reads its options at create: hand it this process's GPU_MAX_HW_QUEUES for
+        # this create only (the option is process-wide; later populations see the old value)
         hwq = _lib.hw_queues_from_env()
+        prev_hwq = _lib.get_engine_option("hw_queues") if hwq is not None else None
         if hwq is not None:
             _lib.set_engine_option("hw_queues", hwq)
         h = ctypes.c_void_p()
-        check(self.lib.fqlpop_create(ctypes.byref(self._c), self.n, fptr(alphas),
-                                     seeds.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
-                                     int(device), ctypes.byref(h)))
+        try:
+            check(self.lib.fqlpop_create(ctypes.byref(self._c), self.n, fptr(alphas),
+                                         seeds.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                         int(device), ctypes.byref(h)))
+        finally:
+            if prev_hwq is not None:
+                _lib.set_engine_option("hw_queues", prev_hwq)
         self._h = h
         self.active = np.ones(self.n, dtype=bool)
         n = ctypes.c_int64()
@@ -380,6 +387,12 @@ class Population:
         check(self.lib.fqlpop_read_probe(self._h, ctypes.byref(tot), ctypes.byref(n), cc))
         mean = tot.value / n.value if n.value else float("nan")
         return mean, int(n.value), (float(cc[0]), float(cc[1]))
+
+    def probe_coverage(self):
+        """(blocks stamped, blocks launched) over the probed launches since set_probe."""
+        seen, exp = ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.fqlpop_probe_coverage(self._h, ctypes.byref(seen), ctypes.byref(exp)))
+        return int(seen.value), int(exp.value)
 
     def dominant_kernel_info(self):
         """(kernel symbol, algorithmic FLOPs, unique HBM bytes) of one launch of

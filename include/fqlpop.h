@@ -96,6 +96,13 @@ const char* fqlpop_last_error(void);
 int fqlpop_set_engine_option(const char* name, int value);
 int fqlpop_get_engine_option(const char* name, int* value);
 int fqlpop_reset_engine_options(void);
+/* Streams (parallel graph branches) a population created now would capture its step on:
+ * 4 (sM, sF, sB, sX), or 1 when engine option serial is set or hw_queues < 4.  The HIP
+ * runtime's graph launch indexes past its branch-stream pool when more branches than
+ * hardware queues share the launch stream's queue; the capture refuses
+ * (FQLPOP_E_STATE) a step with more branches than hw_queues.  No GPU call.  [no reference
+ * counterpart: engine introspection] */
+int fqlpop_step_streams(int* n_streams);
 /* 1 in a diagnostic build (make DIAG=1 / PHASE=1), 0 in the production library. */
 int fqlpop_diagnostic_build(void);
 
@@ -205,6 +212,10 @@ int fqlpop_set_probe(fqlpop_t* h, int enable);
  * launch over the active members. */
 int fqlpop_dominant_kernel_info(fqlpop_t* h, char* name, int name_cap, double* flops, double* bytes);
 int fqlpop_read_probe(fqlpop_t* h, double* total_us, int64_t* launches, double* clock_check);
+/* Probe coverage since set_probe: blocks whose start and end stamps were both written, and
+ * blocks launched, summed over the timed launches (equal when every block of every timed
+ * launch stamped; the stamps are cleared after each read).  [no reference counterpart] */
+int fqlpop_probe_coverage(fqlpop_t* h, int64_t* blocks_seen, int64_t* blocks_expected);
 
 /* ---------------------------------------------------------------------
  * World-model rollout evaluation (BASELINE config 5).

@@ -100,18 +100,103 @@ def test_hw_queues_option_and_env_parse(monkeypatch):
     assert _lib.hw_queues_from_env() is None
 
 
-def test_population_passes_hw_queues_before_create(monkeypatch):
-    """Population hands GPU_MAX_HW_QUEUES to the engine before fqlpop_create (here create
-    then fails: no GPU in the CPU suite), so a caller running the HIP runtime with 2 queues
-    gets the one-stream capture instead of the runtime's crash in hipGraphLaunch."""
+def test_population_passes_hw_queues_for_its_create_only(monkeypatch):
+    """Population hands GPU_MAX_HW_QUEUES to the engine for its own fqlpop_create and then
+    restores the process-wide option: a caller running the HIP runtime with 2
+    queues gets the one-stream capture, and later populations do not inherit the value."""
     import fqlpop
-    from fqlpop import Population, PopulationConfig
+    from fqlpop import Population, PopulationConfig, _lib
+    lib = _lib.load_library()
+    seen = []
+    real = lib.fqlpop_create
+
+    def fake_create(*a):
+        seen.append(fqlpop.get_engine_option("hw_queues"))
+        lib.fqlpop_last_error()  # (keeps the error text path alive)
+        return -1
+
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "2")
+    monkeypatch.setattr(lib, "fqlpop_create", fake_create)
     try:
+        fqlpop.set_engine_option("hw_queues", 8)
         try:
-            Population(PopulationConfig(), [3.0], [1]).close()  # (a GPU host: create succeeds)
+            Population(PopulationConfig(), [3.0], [1]).close()
         except fqlpop.FqlpopError:
             pass
-        assert fqlpop.get_engine_option("hw_queues") == 2
+        assert seen == [2]
+        assert fqlpop.get_engine_option("hw_queues") == 8
+    finally:
+        monkeypatch.setattr(lib, "fqlpop_create", real)
+        fqlpop.reset_engine_options()
+
+
+def test_step_streams_never_exceed_hw_queues():
+    """The hardware-queue invariant: the step is captured on 4 streams
+    only with >= 4 hardware queues, else on one; serial is always one stream."""
+    import fqlpop
+    try:
+        for q in range(1, 17):
+            fqlpop.set_engine_option("hw_queues", q)
+            for serial in (0, 1):
+                fqlpop.set_engine_option("serial", serial)
+                n = fqlpop.step_streams()
+                assert n in (1, 4)
+                assert n == 1 or n <= q
+                assert n == (1 if serial or q < 4 else 4)
     finally:
         fqlpop.reset_engine_options()
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_cpu_allotment_takes_the_smallest_bound(monkeypatch):
+    """The CPU leg's thread count is min(sched_getaffinity, cgroup quota, OMP_NUM_THREADS):
+    the GPU box's affinity mask shows 256 CPUs while the job's share is 16."""
+    b = _bench_module()
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert b.cpu_allotment()["effective_cpus"] == min(3, len(os.sched_getaffinity(0)))
+    monkeypatch.setattr(b, "_cgroup_cpu_quota", lambda: 2)
+    assert b.cpu_allotment()["effective_cpus"] == min(2, len(os.sched_getaffinity(0)))
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    monkeypatch.setattr(b, "_cgroup_cpu_quota", lambda: None)
+    assert b.cpu_allotment()["effective_cpus"] == len(os.sched_getaffinity(0))
+
+
+def test_cpu_baseline_is_bounded_when_oversubscribed():
+    """256 torch threads on this 8-CPU container (32x oversubscribed, the round-4 hang's
+    shape): the leg returns within its wall budget plus one update, never loops on a step
+    floor, and records what it measured or abandoned."""
+    import time
+    import torch
+    b = _bench_module()
+    wl = b.WORKLOADS["cube"]
+    data = b.synthetic_dataset(4096, wl["obs_dim"], wl["action_dim"])
+    prev = torch.get_num_threads()
+    budget = 3.0
+    t0 = time.perf_counter()
+    out = b.cpu_baseline(wl, data, budget, thread_counts=[256])
+    wall = time.perf_counter() - t0
+    assert torch.get_num_threads() == prev
+    one_update = out.get("longest_update_s") or 0.0
+    assert wall <= budget + one_update + 1.0, (wall, out)
+    assert out["leg_s"] <= wall + 0.01
+    if out["value"] is None:
+        assert "256" in out["abandoned"]
+    else:
+        assert out["cores"] == 256 and out["rates_by_threads"]["256"] > 0
+
+
+def test_cpu_baseline_caps_the_whole_leg():
+    """A requested budget above CPU_LEG_CAP_S is clamped to it."""
+    b = _bench_module()
+    wl = b.WORKLOADS["cube"]
+    data = b.synthetic_dataset(4096, wl["obs_dim"], wl["action_dim"])
+    b.CPU_LEG_CAP_S = 1.0
+    out = b.cpu_baseline(wl, data, 1000.0, thread_counts=[2])
+    assert out["budget_s"] == 1.0 and out["leg_s"] < 1.0 + out["longest_update_s"] + 1.0

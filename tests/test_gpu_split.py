@@ -26,15 +26,21 @@ def _data(N, D, A, seed):
             "next_observations": (obs + 0.05 * rng.standard_normal((N, D))).astype(np.float32)}
 
 
-def _run(opts, n_members, D=28, A=5, B=256, steps=3, **kw):
+def _run(opts, n_members, D=28, A=5, B=256, steps=3, probe=False, **kw):
     from fqlpop import Population, PopulationConfig
     alphas = [3.0 * 3.3 ** i for i in range(n_members)]
     with engine_options(**opts):
         pop = Population(PopulationConfig(obs_dim=D, action_dim=A, hidden_dims=(512,) * 4, batch_size=B, **kw),
                          alphas, [11 + i for i in range(n_members)])
         pop.set_dataset(_data(20_000, D, A, 3))
+        if probe:
+            pop.set_probe(True)
         pop.step(steps)
         info = pop.read_info_array().copy()
+        cover = None
+        if probe:
+            cover = (pop.read_probe()[1],) + pop.probe_coverage()
+            pop.set_probe(False)
         rng = np.random.default_rng(9)
         val = {"observations": rng.standard_normal((B, D)).astype(np.float32),
                "actions": rng.uniform(-1, 1, (B, A)).astype(np.float32),
@@ -45,6 +51,8 @@ def _run(opts, n_members, D=28, A=5, B=256, steps=3, **kw):
         flats = [pop.get_flat(i, w) for i in range(n_members) for w in (0, 1, 2)]
         name = pop.dominant_kernel_info()[0]
         pop.close()
+    if probe:
+        return info, vinfo, flats, name, cover
     return info, vinfo, flats, name
 
 
@@ -97,3 +105,19 @@ def test_split_no_error_word_and_probe_times_split_launch():
     name = pop.dominant_kernel_info()[0]
     assert name.startswith("split_fwd_kernel"), name
     pop.close()
+
+
+def test_split_euler_512_blocks_with_probe():
+    """4 members at split_blocks=512 run the Euler flow as 64 tiles x 8
+    blocks = 512 blocks (the launch whose stamps overran round 4's 256-block probe buffer).
+    With the probe on: bit-identical to unsplit, no error word (read_info / sync raise on
+    it), and every block of every timed launch wrote both of its stamps."""
+    steps = 3
+    ref = _run({"split": 0}, 4, steps=steps)
+    got = _run({"split_blocks": 512}, 4, steps=steps, probe=True)
+    assert got[3].startswith("split_fwd_kernel"), got[3]
+    _same(got, ref)
+    launches, seen, expected = got[4]
+    assert launches == steps
+    assert expected == steps * 512, expected
+    assert seen == expected
