@@ -212,10 +212,12 @@ def cpu_baseline(wl: dict, data: dict, budget_s: float, thread_counts=None) -> d
     share = total / len(counts)
     prev_threads = torch.get_num_threads()
     runs, abandoned = {}, {}
+    longest = 0.0
     t_leg = time.perf_counter()
     try:
         for threads in counts:
             r = _cpu_rate(wl, data, share, threads)
+            longest = max(longest, r["longest_update_s"])
             if r["steps"] > 0:
                 runs[threads] = r
             else:
@@ -227,13 +229,14 @@ def cpu_baseline(wl: dict, data: dict, budget_s: float, thread_counts=None) -> d
     if not runs:
         return {"value": None, "unit": "member-grad-steps/s", "cores": None, "kind": "port", "host": host,
                 "rates_by_threads": {}, "abandoned": abandoned, "leg_s": round(leg_s, 2),
+                "longest_update_s": round(longest, 3), "budget_s": round(total, 2),
                 "sample": f"no thread count finished an update within its {share:.1f} s share"}
     best = max(runs, key=lambda t: runs[t]["rate"])
     r = runs[best]
     return {"value": r["rate"], "unit": "member-grad-steps/s", "cores": best, "kind": "port", "host": host,
             "rates_by_threads": {str(t): round(x["rate"], 3) for t, x in runs.items()},
             "abandoned": abandoned, "leg_s": round(leg_s, 2), "budget_s": round(total, 2),
-            "longest_update_s": round(max(x["longest_update_s"] for x in runs.values()), 3),
+            "longest_update_s": round(longest, 3),
             "sample": f"{r['steps']} sequential update() steps of 1 member (alpha=10, B={B}, H=512) in "
                       f"{r['elapsed']:.1f} s after a {r['warmup_s']:.2f} s warm-up update, float32 PyTorch-CPU "
                       f"restatement (oracle/fql_torch.py), torch threads={best}: the best of "

@@ -80,6 +80,8 @@ struct EngineOptions {
     int small_sched = 1;   // small populations (the Euler flow split): target critic and the critic's
                            // TD-column backward on a 4th stream beside the main chain (bit-identical)
     int split_blocks = 256;  // the most blocks of a split forward / Euler launch (F shrinks to fit)
+    int split_sites = 0;   // per-site override of split: 3 bits per launch site (SITE_*: bits 3 site ..),
+                           // 0 auto, 1 unsplit, 2 / 3 / 4 = 2 / 4 / 8 blocks per tile (A/B runs)
     int hw_queues = 4;     // the HIP runtime's hardware queues per process (GPU_MAX_HW_QUEUES, which the
                            // caller sets; the Python layer passes it): below 4 the step is captured on
                            // one stream (graph launch and hardware queues)
@@ -116,6 +118,7 @@ const EngineOptionRef kEngineOptions[] = {
     {"split", &EngineOptions::split, 0, 8},
     {"small_sched", &EngineOptions::small_sched, 0, 1},
     {"hw_queues", &EngineOptions::hw_queues, 1, 1024},
+    {"split_sites", &EngineOptions::split_sites, 0, (1 << 24) - 1},
     {"split_blocks", &EngineOptions::split_blocks, 64, 1024},
 };
 
@@ -563,31 +566,94 @@ void gemm(int layout, int epi, const GemmArgs& g, hipStream_t s) {
 }
 
 // Split launch sites (fqlpop::split_site): BC forward, Euler flow (sF); one-step, target
-// critic, critic forwards (sM).
-// critic and one-step backwards (sM).  The BC backward (sB) stays unsplit: at most two split
-// launches (one per stream of sF, sM) can then run at once.
-// (SITE_CRB2: the critic's TD-column backward on sX in the small-population schedule)
+// critic, critic forwards, critic and one-step backwards (sM); in the small-population
+// schedule the target critic and the critic's TD-column backward (SITE_CRB2) run on sX.  The
+// BC backward (sB) stays unsplit.
 enum { SITE_BCF = 0, SITE_EULER = 1, SITE_OSF = 2, SITE_TGT = 3, SITE_CRF = 4, SITE_CRB = 5, SITE_OSB = 6, SITE_CRB2 = 7,
        SITE_N = 8 };
-constexpr long long kSplitMaxClusters = 128;  // a site with more 16-column tiles runs unsplit
-constexpr long long kSplitMaxBlocks = 256;    // one block per CU (see split_factor)
+constexpr long long kSplitMaxClusters = 128;     // a forward site with more 16-column tiles runs unsplit
+constexpr long long kSplitMaxClustersBwd = 64;   // the one-step backward: above this, unsplit is faster
+constexpr long long kSplitMaxBlocks = 256;       // one block per CU (see split_factor)
 
 // Blocks per 16-column tile of a split launch (1 = the unsplit kernel).  Only where the
-// unsplit kernel leaves CUs idle (<= 128 tiles); the most of 8, 4, 2 blocks that keeps the
-// launch within 256 blocks (forced values shrink to fit).  The split kernel runs 2 waves per
-// SIMD and <= 59 KB of LDS per block, so the split launches of the two streams that can run
-// at once (sF, sM) fit the chip together; the blocks take their clusters by ticket, in the
-// order they become resident (kernels.hip, sp_ticket), so a cluster never waits for blocks
-// that cannot be scheduled.  The Euler flow and the LN backward use 4 or 8 blocks (their
-// 2-block forms would spill).
-int split_factor(const fqlpop* h, long long clusters, bool min4, long long max_blocks = kSplitMaxBlocks) {
-    const int opt = h->opt.split;
-    if (!h->split_ok || opt == 0 || clusters > kSplitMaxClusters) return 1;
+// unsplit kernel leaves CUs idle (<= 128 tiles, <= 64 for the one-step backward); the most of
+// 8, 4, 2 blocks that keeps the launch within 256 blocks (forced values shrink to fit).  The
+// Euler flow and the LN backward use 4 or 8 blocks (their 2-block forms would spill).
+// Residency: a split kernel takes 200-256 VGPRs (2 waves per SIMD) for its 4 waves, so the
+// chip holds 512 split blocks at once, and up to three split launches (sF, sM, sX) can be in
+// flight together, more blocks than fit.  Progress does not depend on a budget: every launch's
+// blocks take their clusters by ticket in the order they become resident (kernels.hip,
+// sp_begin), so each launch has at most one partly resident cluster (<= 7 blocks) and all its
+// other clusters can finish and free their CUs, whatever else runs (the hand-off waits give
+// up after ~2 s and set the error word otherwise).  The budgets are for speed: same-box A/B
+//  put the critic's LN backward at 256 blocks (F = 4 at 2 members, 8 at
+// 1) and the one-step backward unsplit from 128 tiles (8 members).
+int split_factor_opts(const EngineOptions& o, bool split_ok, int site, long long clusters, bool min4,
+                      long long max_blocks) {
+    int opt = o.split;
+    const int code = (o.split_sites >> (3 * site)) & 7;
+    if (code == 1) return 1;
+    if (code >= 2 && code <= 4) {
+        opt = 1 << (code - 1);
+        max_blocks = std::max<long long>(max_blocks, clusters * opt);  // (a forced F is not shrunk)
+    }
+    if (!split_ok || opt == 0 || clusters > (site == SITE_OSB ? kSplitMaxClustersBwd : kSplitMaxClusters)) return 1;
     for (int F = std::max(opt >= 2 ? opt : 8, min4 ? 4 : 2); F >= 2; F /= 2) {
         if (min4 && F < 4) break;
         if (clusters * F <= max_blocks) return F;
     }
     return 1;
+}
+int split_factor(const fqlpop* h, int site, long long clusters, bool min4, long long max_blocks = kSplitMaxBlocks) {
+    return split_factor_opts(h->opt, h->split_ok, site, clusters, min4, max_blocks);
+}
+
+// The split plan of a step over nz members: F per launch site (1 = unsplit) and whether the
+// small-population schedule runs, from the shapes and engine options alone (no GPU).  The
+// launches compute their F at the call sites (stream_fwd, euler_split, bwd_split) and check it
+// against this plan, so the plan that fqlpop_split_plan reports is the one that runs.
+struct SplitShape {
+    int H, L, A, B, E, K0bc, K0os, K0cr;
+    bool critic_ln, stream_fwd, stream_bwd, fused_adam, euler_fused, multi_stream;
+};
+void split_plan(const EngineOptions& o, const SplitShape& d, int nz, int F[SITE_N], bool* small) {
+    const bool ok = d.stream_fwd && o.split != 0;
+    const int B = d.B, B2 = 2 * B, B3 = 3 * B, T = B / 16;
+    auto fwd = [&](int site, int K0, int nout, int M, long long clusters, bool min4) {
+        F[site] = d.stream_fwd && split_fwd_supported(d.H, d.L, K0, nout, M)
+                      ? split_factor_opts(o, ok, site, clusters, min4, o.split_blocks) : 1;
+    };
+    fwd(SITE_EULER, d.K0bc, d.A, B, (long long)T * nz, true);
+    if (!d.euler_fused) F[SITE_EULER] = 1;
+    *small = o.small_sched && d.multi_stream && d.stream_fwd && d.stream_bwd && d.fused_adam && F[SITE_EULER] == 8;
+    fwd(SITE_BCF, d.K0bc, d.A, B2, (long long)(B2 / 16) * nz, false);
+    fwd(SITE_OSF, d.K0os, d.A, B3, (long long)(B3 / 16) * nz, false);
+    fwd(SITE_TGT, d.K0cr, 1, B, (long long)T * d.E * nz, false);
+    fwd(SITE_CRF, d.K0cr, 1, B2, (long long)(B2 / 16) * d.E * nz, false);
+    auto bwd = [&](int site, int nout, int M, int Mg, long long clusters, bool min4) {
+        F[site] = d.stream_bwd && split_bwd_supported(d.H, d.L, nout, M, Mg)
+                      ? split_factor_opts(o, ok, site, clusters, min4, kSplitMaxBlocks) : 1;
+    };
+    if (*small) {
+        bwd(SITE_CRB, 1, B, 0, (long long)T * d.E * nz, d.critic_ln);  // the Q-loss columns
+        bwd(SITE_CRB2, 1, B, B, (long long)T * d.E * nz, d.critic_ln);  // the TD columns (sX)
+    } else {
+        bwd(SITE_CRB, 1, B2, B, (long long)(B2 / 16) * d.E * nz, d.critic_ln);
+        F[SITE_CRB2] = 1;
+    }
+    bwd(SITE_OSB, d.A, B, B, (long long)T * nz, false);
+}
+SplitShape split_shape(const fqlpop* h) {
+    return SplitShape{h->H, h->L, h->A, h->B, h->E, h->bc.in_dim, h->os.in_dim, h->critic.in_dim, h->critic.ln,
+                      h->stream_fwd, h->stream_bwd, h->fused_adam, h->euler_fused, h->sX != h->sM};
+}
+// the call site's F against the plan (a divergence would make fqlpop_split_plan report a
+// schedule that does not run)
+void check_plan(const fqlpop* h, int site, int nz, int F) {
+    int plan[SITE_N];
+    bool small = false;
+    split_plan(h->opt, split_shape(h), nz, plan, &small);
+    ARGCHK(plan[site] == F, "split launch differs from the split plan");
 }
 
 // The site's synchronisation state for one launch over `clusters` tiles.  Its counters (per
@@ -603,9 +669,9 @@ SplitSync split_prep(fqlpop* h, int site, long long clusters, hipStream_t) {
 // Blocks per tile of a streamed backward launch (1 = unsplit): the critic (LN: its 2-block
 // form would spill, so 4 or 8, up to 2 blocks per CU: 4 x 128 tiles for a 2-member
 // population) and the one-step actor on sM; never the BC actor on sB.
-int bwd_split(const fqlpop* h, const NetLayout& N, int M, int Mg, int nz) {
+int bwd_split(const fqlpop* h, int site, const NetLayout& N, int M, int Mg, int nz) {
     if (&N == &h->bc || !split_bwd_supported(N.H, N.L, N.out_dim, M, Mg)) return 1;
-    return split_factor(h, (long long)(M / 16) * N.E * nz, N.ln, N.ln ? 2 * kSplitMaxBlocks : kSplitMaxBlocks);
+    return split_factor(h, site, (long long)(M / 16) * N.E * nz, N.ln, kSplitMaxBlocks);
 }
 
 // Forward of the hidden stack of `N` over `M` columns of input X (ld = ldx).
@@ -794,10 +860,11 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
         a.phase = h->phase_dev;
     }
     if (!(skip_mask() & (&N == &h->critic ? 32 : &N == &h->bc ? 64 : 128))) {
-        const int F = bwd_split(h, N, M, Mg, c.nz);
+        const int site = &N != &h->critic ? SITE_OSB : (s == h->sX && h->sX != h->sM) ? SITE_CRB2 : SITE_CRB;
+        const int F = bwd_split(h, site, N, M, Mg, c.nz);
+        if (&N != &h->bc) check_plan(h, site, c.nz, F);
         if (F > 1) {
             const long long clusters = (long long)(M / 16) * N.E * c.nz;
-            const int site = &N != &h->critic ? SITE_OSB : (s == h->sX && h->sX != h->sM) ? SITE_CRB2 : SITE_CRB;
             launch_split_bwd(N.ln, F, a, split_prep(h, site, clusters, s), s);
         } else {
             launch_stream_bwd(N.ln, a, s);
@@ -983,7 +1050,8 @@ void stream_fwd(const Ctx& c, hipStream_t s, const NetLayout& N, const float* ar
     if (sk & bit) return;
     const int site = &N == &h->bc ? SITE_BCF : &N == &h->os ? SITE_OSF : arena == h->target ? SITE_TGT : SITE_CRF;
     const long long clusters = (long long)(M / 16) * N.E * c.nz;
-    const int F = split_fwd_supported(N.H, N.L, N.in_dim, N.out_dim, M) ? split_factor(h, clusters, false, h->opt.split_blocks) : 1;
+    const int F = split_fwd_supported(N.H, N.L, N.in_dim, N.out_dim, M) ? split_factor(h, site, clusters, false, h->opt.split_blocks) : 1;
+    check_plan(h, site, c.nz, F);
     if (F > 1) {
         SplitFwdArgs sa{};
         sa.s = a;
@@ -998,7 +1066,7 @@ void stream_fwd(const Ctx& c, hipStream_t s, const NetLayout& N, const float* ar
 int euler_split(const fqlpop* h, int nz) {
     const NetLayout& N = h->bc;
     if (!h->euler_fused || !split_fwd_supported(N.H, N.L, N.in_dim, N.out_dim, h->B)) return 1;
-    return split_factor(h, (long long)(h->B / 16) * nz, true, h->opt.split_blocks);
+    return split_factor(h, SITE_EULER, (long long)(h->B / 16) * nz, true, h->opt.split_blocks);
 }
 SplitFwdArgs euler_split_args(fqlpop* h, const EulerArgs& ea, hipStream_t s) {
     const NetLayout& N = h->bc;
@@ -1359,8 +1427,16 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     // stream sX beside the main chain, which then carries the critic forward, the Q-loss
     // columns' backward (dQ/da) and the actor chain only.  sX forks from sM and joins sM / sB;
     // it never waits on sB or sF (capture rule above).
+    // (only with the Euler flow at 8 blocks per tile, i.e. <= 16 tiles: cube, 1-2 members; at
+    // 4 blocks per tile the 4th stream measured 12-14 % slower)
     const bool small = h->opt.small_sched && h->sX != h->sM && h->stream_fwd && h->stream_bwd && h->fused_adam &&
-                       euler_split(h, c.nz) > 1;
+                       euler_split(h, c.nz) == 8;
+    {
+        int plan[SITE_N];
+        bool plan_small = false;
+        split_plan(h->opt, split_shape(h), c.nz, plan, &plan_small);
+        ARGCHK(plan_small == small && plan[SITE_EULER] == euler_split(h, c.nz), "step differs from the split plan");
+    }
     hipStream_t sT = small ? h->sX : sM;
     dep(sM, sT);  // a' is in the target-critic input
     // ---- sM (sX): target critic on [s', a'] (params from the target arena) -----
@@ -1706,6 +1782,25 @@ int fqlpop_get_engine_option(const char* name, int* value) {
 
 int fqlpop_reset_engine_options(void) {
     return guard([&] { g_engine_opts = EngineOptions{}; });
+}
+
+int fqlpop_split_plan(const fqlpop_config* cfg, int n_members, int* blocks_per_tile, int* small_sched) {
+    return guard([&] {
+        ARGCHK(cfg && blocks_per_tile && small_sched && n_members >= 1, "bad argument");
+        const EngineOptions& eo = g_engine_opts;
+        const int D = cfg->obs_dim, A = cfg->action_dim, B = cfg->batch_size, H = cfg->hidden_dim, L = cfg->num_hidden;
+        SplitShape d{H, L, A, B, cfg->num_qs, D + A + 1, D + A, D + A, cfg->layer_norm != 0,
+                     stream_fwd_supported(H, L, D + A + 1, A, B) && eo.stream_fwd != 0,
+                     stream_bwd_supported(H, L, A, B, B) && eo.stream_bwd != 0, false,
+                     euler_flow_supported(H, L, D, A, B) && !cfg->actor_layer_norm && eo.euler_fused != 0,
+                     step_streams(eo) > 1};
+        d.fused_adam = d.stream_bwd && H % 128 == 0 && L <= GEMM_GROUP_MAX && eo.fused_adam;
+        int F[SITE_N];
+        bool small = false;
+        split_plan(eo, d, n_members, F, &small);
+        for (int i = 0; i < SITE_N; ++i) blocks_per_tile[i] = F[i];
+        *small_sched = small ? 1 : 0;
+    });
 }
 
 int fqlpop_step_streams(int* n_streams) {

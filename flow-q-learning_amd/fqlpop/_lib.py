@@ -84,6 +84,8 @@ _SIGS = {
     "fqlpop_reset_engine_options": (ctypes.c_int, []),
     "fqlpop_diagnostic_build": (ctypes.c_int, []),
     "fqlpop_step_streams": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "fqlpop_split_plan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                         ctypes.POINTER(ctypes.c_int)]),
     "fqlpop_probe_coverage": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
                                              ctypes.POINTER(ctypes.c_int64)]),
     "fqlpop_create": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.c_int, _F,

@@ -80,6 +80,23 @@ def _f32(a) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
 
 
+SPLIT_SITES = ("bc_forward", "euler_flow", "onestep_forward", "target_critic", "critic_forward", "critic_backward",
+               "onestep_backward", "critic_backward_td")
+
+
+def split_plan(cfg: "PopulationConfig", n_members: int) -> dict:
+    """The split plan (fqlpop_split_plan; no GPU call) of an n_members population with
+    ``cfg`` under the current engine options: blocks per 16-column tile per launch site
+    (1 = unsplit) and whether the small-population schedule runs."""
+    c = cfg.to_c()
+    F = (ctypes.c_int * 8)()
+    small = ctypes.c_int()
+    check(_lib.load_library().fqlpop_split_plan(ctypes.byref(c), int(n_members), F, ctypes.byref(small)))
+    out = dict(zip(SPLIT_SITES, [int(x) for x in F]))
+    out["small_sched"] = bool(small.value)
+    return out
+
+
 class Population:
     """A population of FQL agents (one alpha and seed per member) on one GPU."""
 

@@ -96,6 +96,14 @@ const char* fqlpop_last_error(void);
 int fqlpop_set_engine_option(const char* name, int value);
 int fqlpop_get_engine_option(const char* name, int* value);
 int fqlpop_reset_engine_options(void);
+/* The split plan a population of n_members created now with `cfg` would run (no GPU call):
+ * blocks per 16-column tile of each split launch site, 1 = the unsplit kernel, in site order
+ * {BC forward, Euler flow, one-step forward, target critic, critic forward, critic backward
+ * (its Q-loss columns under the small-population schedule), one-step backward, critic
+ * TD-column backward (small-population schedule only)} (blocks_per_tile[8]), and whether the
+ * small-population schedule (4th stream) runs.  The step checks each launch against this plan.
+ * [no reference counterpart: engine introspection] */
+int fqlpop_split_plan(const fqlpop_config* cfg, int n_members, int* blocks_per_tile, int* small_sched);
 /* Streams (parallel graph branches) a population created now would capture its step on:
  * 4 (sM, sF, sB, sX), or 1 when engine option serial is set or hw_queues < 4.  The HIP
  * runtime's graph launch indexes past its branch-stream pool when more branches than

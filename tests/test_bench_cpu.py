@@ -200,3 +200,56 @@ def test_cpu_baseline_caps_the_whole_leg():
     b.CPU_LEG_CAP_S = 1.0
     out = b.cpu_baseline(wl, data, 1000.0, thread_counts=[2])
     assert out["budget_s"] == 1.0 and out["leg_s"] < 1.0 + out["longest_update_s"] + 1.0
+
+
+def _plan(members, **cfg):
+    from fqlpop import PopulationConfig, split_plan
+    base = dict(obs_dim=28, action_dim=5, hidden_dims=(512,) * 4, batch_size=256)
+    base.update(cfg)
+    return split_plan(PopulationConfig(**base), members)
+
+
+def test_split_plan_per_members_and_workload():
+    """The split plan chosen from same-box A/B runs (DESIGN.md section 6,
+    profiles/round5c): cube at 1-2 members splits every launch with the 4th stream; at 2 members
+    the critic's LN backward takes 4 blocks per tile (256 blocks, not 512); at 4 members the
+    Euler flow runs at 4 blocks per tile without the 4th stream (12-14 % faster than with it);
+    from 8 members only nothing splits (the one-step backward at 128 tiles measured 2.4 %
+    slower split).  antsoccer (B = 1024): one member splits without the 4th stream, two
+    members run unsplit."""
+    import fqlpop
+    fqlpop.reset_engine_options()
+    p = _plan(1)
+    assert p["small_sched"] and p["euler_flow"] == 8 and p["critic_backward"] == 8 and p["critic_backward_td"] == 8
+    assert p["onestep_backward"] == 8 and p["critic_forward"] == 4 and p["onestep_forward"] == 4
+    p = _plan(2)
+    assert p["small_sched"] and p["euler_flow"] == 8
+    assert p["critic_backward"] == 4 and p["critic_backward_td"] == 4
+    assert p["critic_forward"] == 2 and p["target_critic"] == 4 and p["onestep_backward"] == 8
+    p = _plan(4)
+    assert not p["small_sched"] and p["euler_flow"] == 4 and p["critic_backward_td"] == 1
+    assert p["onestep_backward"] == 4 and p["critic_forward"] == 1 and p["critic_backward"] == 1
+    for m in (8, 16):
+        p = _plan(m)
+        assert not p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES), (m, p)
+    p = _plan(1, obs_dim=42, action_dim=8, batch_size=1024)
+    assert not p["small_sched"] and p["euler_flow"] == 4 and p["critic_backward_td"] == 1
+    p = _plan(2, obs_dim=42, action_dim=8, batch_size=1024)
+    assert not p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES), p
+
+
+def test_split_plan_follows_engine_options():
+    import fqlpop
+    try:
+        fqlpop.set_engine_option("split", 0)
+        p = _plan(1)
+        assert not p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES)
+        fqlpop.reset_engine_options()
+        fqlpop.set_engine_option("split_sites", 1 << 3)  # the Euler flow unsplit: no 4th stream
+        p = _plan(2)
+        assert p["euler_flow"] == 1 and not p["small_sched"] and p["onestep_forward"] > 1
+        fqlpop.reset_engine_options()
+        fqlpop.set_engine_option("serial", 1)  # one stream: no small-population schedule
+        assert not _plan(2)["small_sched"]
+    finally:
+        fqlpop.reset_engine_options()

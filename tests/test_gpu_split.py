@@ -121,3 +121,4 @@ def test_split_euler_512_blocks_with_probe():
     assert launches == steps
     assert expected == steps * 512, expected
     assert seen == expected
+
