@@ -571,12 +571,20 @@ void gemm(int layout, int epi, const GemmArgs& g, hipStream_t s) {
 // BC backward (sB) stays unsplit.
 enum { SITE_BCF = 0, SITE_EULER = 1, SITE_OSF = 2, SITE_TGT = 3, SITE_CRF = 4, SITE_CRB = 5, SITE_OSB = 6, SITE_CRB2 = 7,
        SITE_N = 8 };
-constexpr long long kSplitMaxClusters = 128;     // a forward site with more 16-column tiles runs unsplit
-constexpr long long kSplitMaxClustersBwd = 64;   // the one-step backward: above this, unsplit is faster
+// a site with more 16-column tiles than its cap runs unsplit (same-box A/B, DESIGN.md section 5,
+// round 5): 128 for the Euler flow, the one-step forward (the chain's first launch) and the
+// critic's LN backward, 64 for the BC forward, the target critic, the critic forward and the
+// one-step backward (at 96-128 tiles their unsplit kernels were 3-5 % faster in the step)
+constexpr long long kSplitMaxClusters = 128;
+constexpr long long kSplitMaxClustersSide = 64;
+constexpr long long split_cap(int site) {
+    return (site == SITE_BCF || site == SITE_TGT || site == SITE_CRF || site == SITE_OSB) ? kSplitMaxClustersSide
+                                                                                        : kSplitMaxClusters;
+}
 constexpr long long kSplitMaxBlocks = 256;       // one block per CU (see split_factor)
 
 // Blocks per 16-column tile of a split launch (1 = the unsplit kernel).  Only where the
-// unsplit kernel leaves CUs idle (<= 128 tiles, <= 64 for the one-step backward); the most of
+// unsplit kernel leaves CUs idle (<= split_cap tiles); the most of
 // 8, 4, 2 blocks that keeps the launch within 256 blocks (forced values shrink to fit).  The
 // Euler flow and the LN backward use 4 or 8 blocks (their 2-block forms would spill).
 // Residency: a split kernel takes 200-256 VGPRs (2 waves per SIMD) for its 4 waves, so the
@@ -587,7 +595,7 @@ constexpr long long kSplitMaxBlocks = 256;       // one block per CU (see split_
 // other clusters can finish and free their CUs, whatever else runs (the hand-off waits give
 // up after ~2 s and set the error word otherwise).  The budgets are for speed: same-box A/B
 //  put the critic's LN backward at 256 blocks (F = 4 at 2 members, 8 at
-// 1) and the one-step backward unsplit from 128 tiles (8 members).
+// 1), the one-step backward unsplit from 128 tiles (8 members) and the side forwards from 96.
 int split_factor_opts(const EngineOptions& o, bool split_ok, int site, long long clusters, bool min4,
                       long long max_blocks) {
     int opt = o.split;
@@ -597,7 +605,7 @@ int split_factor_opts(const EngineOptions& o, bool split_ok, int site, long long
         opt = 1 << (code - 1);
         max_blocks = std::max<long long>(max_blocks, clusters * opt);  // (a forced F is not shrunk)
     }
-    if (!split_ok || opt == 0 || clusters > (site == SITE_OSB ? kSplitMaxClustersBwd : kSplitMaxClusters)) return 1;
+    if (!split_ok || opt == 0 || clusters > split_cap(site)) return 1;
     for (int F = std::max(opt >= 2 ? opt : 8, min4 ? 4 : 2); F >= 2; F /= 2) {
         if (min4 && F < 4) break;
         if (clusters * F <= max_blocks) return F;
@@ -1312,6 +1320,24 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     sa.rew_t = tref(h->rew_t, B);
     sa.mask_t = tref(h->mask_t, B);
     sa.nz = c.nz; sa.slots = h->slots;
+    // one-step actor forward on [s'; s; s] (z_next; z_d; z_metric), on sM
+    auto os_forward = [&]() {
+        const NetLayout& N = h->os;
+        HeadArgs ha = head_args(c, N, h->os_g[L - 1], B3, B3, 0);
+        ha.o0 = tref(h->apiraw, (long long)A * B); ha.ld0 = B;
+        ha.o1 = tref(h->tg_in, (long long)Kc * B); ha.ld1 = B;
+        ha.o2 = tref(h->cr_in, (long long)Kc * B2); ha.ld2 = B2;
+        ha.o3 = tref(h->amet, (long long)A * B); ha.ld3 = B;
+        if (h->stream_fwd) {
+            // only the z_d rows [B, 2B) are back-propagated (distill + Q loss)
+            stream_fwd(c, sM, N, h->params, h->P, tref(h->os_in, (long long)Kc * B3), B3, B3, &h->os_u, &h->os_g,
+                       nullptr, nullptr, (long long)H * B3, 0, 0, 0, B, 2 * B, HEAD_OS, ha);
+        } else {
+            fwd_hidden(c, sM, N, tref(h->os_in, (long long)Kc * B3), B3, B3, h->os_u, h->os_g, 0,
+                       nullptr, nullptr, 0, true);
+            launch_head_fwd(HEAD_OS, ha, sM);
+        }
+    };
     launch_sample(sa, sM);
     HIPCHK(hipEventRecord(h->ev_sample, sM));
     if (sF != sM) HIPCHK(hipStreamWaitEvent(sF, h->ev_sample, 0));
@@ -1403,23 +1429,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     HIPCHK(hipEventRecord(h->ev_bdone, sB));
 
     // ---- sM: one-step actor forward on [s'; s; s] (z_next; z_d; z_metric) --
-    {
-        const NetLayout& N = h->os;
-        HeadArgs ha = head_args(c, N, h->os_g[L - 1], B3, B3, 0);
-        ha.o0 = tref(h->apiraw, (long long)A * B); ha.ld0 = B;
-        ha.o1 = tref(h->tg_in, (long long)Kc * B); ha.ld1 = B;
-        ha.o2 = tref(h->cr_in, (long long)Kc * B2); ha.ld2 = B2;
-        ha.o3 = tref(h->amet, (long long)A * B); ha.ld3 = B;
-        if (h->stream_fwd) {
-            // only the z_d rows [B, 2B) are back-propagated (distill + Q loss)
-            stream_fwd(c, sM, N, h->params, h->P, tref(h->os_in, (long long)Kc * B3), B3, B3, &h->os_u, &h->os_g,
-                       nullptr, nullptr, (long long)H * B3, 0, 0, 0, B, 2 * B, HEAD_OS, ha);
-        } else {
-            fwd_hidden(c, sM, N, tref(h->os_in, (long long)Kc * B3), B3, B3, h->os_u, h->os_g, 0,
-                       nullptr, nullptr, 0, true);
-            launch_head_fwd(HEAD_OS, ha, sM);
-        }
-    }
+    os_forward();
     const NetLayout& NC = h->critic;
     const long long sy2 = (long long)H * B2, sy1 = (long long)H * B;
     // Small populations (the Euler flow runs split: DESIGN.md section 4, small-population

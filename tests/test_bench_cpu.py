@@ -214,9 +214,11 @@ def test_split_plan_per_members_and_workload():
     profiles/round5c): cube at 1-2 members splits every launch with the 4th stream; at 2 members
     the critic's LN backward takes 4 blocks per tile (256 blocks, not 512); at 4 members the
     Euler flow runs at 4 blocks per tile without the 4th stream (12-14 % faster than with it);
-    from 8 members only nothing splits (the one-step backward at 128 tiles measured 2.4 %
-    slower split).  antsoccer (B = 1024): one member splits without the 4th stream, two
-    members run unsplit."""
+    from 8 members nothing splits (the one-step backward at 128 tiles measured 2.4 % slower
+    split); the BC forward, target critic and critic forward run unsplit from 96 tiles (3-5 %
+    faster), the one-step forward (the chain's first launch) splits up to 128.  antsoccer
+    (B = 1024): one member splits the flow and the one-step backward, two members run
+    unsplit."""
     import fqlpop
     fqlpop.reset_engine_options()
     p = _plan(1)
@@ -225,15 +227,18 @@ def test_split_plan_per_members_and_workload():
     p = _plan(2)
     assert p["small_sched"] and p["euler_flow"] == 8
     assert p["critic_backward"] == 4 and p["critic_backward_td"] == 4
-    assert p["critic_forward"] == 2 and p["target_critic"] == 4 and p["onestep_backward"] == 8
+    assert p["critic_forward"] == 1 and p["target_critic"] == 4 and p["onestep_backward"] == 8
+    assert p["onestep_forward"] == 2 and p["bc_forward"] == 4
     p = _plan(4)
     assert not p["small_sched"] and p["euler_flow"] == 4 and p["critic_backward_td"] == 1
     assert p["onestep_backward"] == 4 and p["critic_forward"] == 1 and p["critic_backward"] == 1
+    assert p["bc_forward"] == 1 and p["target_critic"] == 1
     for m in (8, 16):
         p = _plan(m)
         assert not p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES), (m, p)
     p = _plan(1, obs_dim=42, action_dim=8, batch_size=1024)
     assert not p["small_sched"] and p["euler_flow"] == 4 and p["critic_backward_td"] == 1
+    assert p["bc_forward"] == 1 and p["target_critic"] == 1 and p["onestep_backward"] == 4
     p = _plan(2, obs_dim=42, action_dim=8, batch_size=1024)
     assert not p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES), p
 
