@@ -258,3 +258,34 @@ def test_split_plan_follows_engine_options():
         assert not _plan(2)["small_sched"]
     finally:
         fqlpop.reset_engine_options()
+
+
+def test_cgroup_quota_parsing(monkeypatch, tmp_path):
+    """cgroup v2 cpu.max ("quota period" or "max period") and v1 cfs_quota_us / cfs_period_us
+    (-1 = none), rounded up to whole CPUs."""
+    import builtins
+    b = _bench_module()
+    files = {}
+    real_open = builtins.open
+
+    def fake_open(p, *a, **k):
+        if p in files:
+            f = tmp_path / p.replace("/", "_")
+            f.write_text(files[p])
+            return real_open(f, *a, **k)
+        if str(p).startswith("/sys/fs/cgroup"):
+            raise OSError("absent")
+        return real_open(p, *a, **k)
+
+    monkeypatch.setattr(builtins, "open", fake_open)
+    files.update({"/sys/fs/cgroup/cpu.max": "1600000 100000\n"})
+    assert b._cgroup_cpu_quota() == 16
+    files["/sys/fs/cgroup/cpu.max"] = "150000 100000\n"
+    assert b._cgroup_cpu_quota() == 2
+    files["/sys/fs/cgroup/cpu.max"] = "max 100000\n"
+    assert b._cgroup_cpu_quota() is None
+    del files["/sys/fs/cgroup/cpu.max"]
+    files.update({"/sys/fs/cgroup/cpu/cpu.cfs_quota_us": "800000\n", "/sys/fs/cgroup/cpu/cpu.cfs_period_us": "100000\n"})
+    assert b._cgroup_cpu_quota() == 8
+    files["/sys/fs/cgroup/cpu/cpu.cfs_quota_us"] = "-1\n"
+    assert b._cgroup_cpu_quota() is None

@@ -122,3 +122,33 @@ def test_split_euler_512_blocks_with_probe():
     assert expected == steps * 512, expected
     assert seen == expected
 
+
+
+def _prune_revive(opts):
+    from fqlpop import Population, PopulationConfig
+    with engine_options(**opts):
+        pop = Population(PopulationConfig(hidden_dims=(512,) * 4, batch_size=256), [3.0, 30.0, 300.0], [4, 5, 6])
+        pop.set_dataset(_data(20_000, 28, 5, 6))
+        pop.step(3)
+        pop.set_active([1, 0, 1])  # fewer clusters per split launch
+        pop.step(2)
+        pop.set_active([1, 1, 1])  # more again: exchange words of the dropped clusters were cleared
+        pop.step(2)
+        pop.sync()
+        out = ([pop.get_flat(i, w) for i in range(3) for w in (0, 1, 2)], [pop.get_count(i) for i in range(3)],
+               pop.read_info_array().copy())
+        pop.close()
+    return out
+
+
+def test_prune_and_revive_split_bit_identical():
+    """A member dropped and revived (SuccessiveHalving's pruning, the distributed trainer's
+    member moves) changes the number of clusters of every split launch twice; the split run
+    stays bit-identical to the unsplit one, no hand-off wait gives up, and get_state /
+    get_count (which now refuse state a failed split launch wrote) return normally."""
+    ref = _prune_revive({"split": 0})
+    got = _prune_revive({})
+    assert got[1] == ref[1] == [7, 5, 7]
+    assert np.array_equal(got[2], ref[2])
+    for i, (x, y) in enumerate(zip(got[0], ref[0])):
+        assert np.array_equal(x, y), f"state {i} differs"
