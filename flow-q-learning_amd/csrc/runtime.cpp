@@ -77,8 +77,8 @@ struct EngineOptions {
     int adam_nt = 3;       // non-temporal optimiser streams (AdamEpi::nt bit mask)
     int split = 1;         // small populations: streamed forwards / Euler flow as clusters of 2-8 blocks per
                            // 16-column tile (bit-identical); 0 off, 1 auto, 2 / 4 / 8 blocks where they fit
-    int small_sched = 1;   // small populations (the Euler flow split): target critic and the critic's
-                           // TD-column backward on a 4th stream beside the main chain (bit-identical)
+    int small_sched = 1;   // the 4th-stream schedule: target critic and the critic's TD-column backward on
+                           // a 4th stream sX beside the main chain (bit-identical); 0 = three streams
     int split_blocks = 256;  // the most blocks of a split forward / Euler launch (F shrinks to fit)
     int split_sites = 0;   // per-site override of split: 3 bits per launch site (SITE_*: bits 3 site ..),
                            // 0 auto, 1 unsplit, 2 / 3 / 4 = 2 / 4 / 8 blocks per tile (A/B runs)
@@ -566,8 +566,8 @@ void gemm(int layout, int epi, const GemmArgs& g, hipStream_t s) {
 }
 
 // Split launch sites (fqlpop::split_site): BC forward, Euler flow (sF); one-step, target
-// critic, critic forwards, critic and one-step backwards (sM); in the small-population
-// schedule the target critic and the critic's TD-column backward (SITE_CRB2) run on sX.  The
+// critic, critic forwards, critic and one-step backwards (sM); in the 4th-stream schedule
+// the target critic and the critic's TD-column backward (SITE_CRB2) run on sX.  The
 // BC backward (sB) stays unsplit.
 enum { SITE_BCF = 0, SITE_EULER = 1, SITE_OSF = 2, SITE_TGT = 3, SITE_CRF = 4, SITE_CRB = 5, SITE_OSB = 6, SITE_CRB2 = 7,
        SITE_N = 8 };
@@ -617,7 +617,7 @@ int split_factor(const fqlpop* h, int site, long long clusters, bool min4, long 
 }
 
 // The split plan of a step over nz members: F per launch site (1 = unsplit) and whether the
-// small-population schedule runs, from the shapes and engine options alone (no GPU).  The
+// 4th-stream schedule runs, from the shapes and engine options alone (no GPU).  The
 // launches compute their F at the call sites (stream_fwd, euler_split, bwd_split) and check it
 // against this plan, so the plan that fqlpop_split_plan reports is the one that runs.
 struct SplitShape {
@@ -633,7 +633,7 @@ void split_plan(const EngineOptions& o, const SplitShape& d, int nz, int F[SITE_
     };
     fwd(SITE_EULER, d.K0bc, d.A, B, (long long)T * nz, true);
     if (!d.euler_fused) F[SITE_EULER] = 1;
-    *small = o.small_sched && d.multi_stream && d.stream_fwd && d.stream_bwd && d.fused_adam && F[SITE_EULER] == 8;
+    *small = o.small_sched && d.multi_stream && d.stream_fwd && d.stream_bwd && d.fused_adam;
     fwd(SITE_BCF, d.K0bc, d.A, B2, (long long)(B2 / 16) * nz, false);
     fwd(SITE_OSF, d.K0os, d.A, B3, (long long)(B3 / 16) * nz, false);
     fwd(SITE_TGT, d.K0cr, 1, B, (long long)T * d.E * nz, false);
@@ -1432,15 +1432,14 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     os_forward();
     const NetLayout& NC = h->critic;
     const long long sy2 = (long long)H * B2, sy1 = (long long)H * B;
-    // Small populations (the Euler flow runs split: DESIGN.md section 4, small-population
-    // schedule): the target critic and, later, the critic's TD-column backward run on a 4th
-    // stream sX beside the main chain, which then carries the critic forward, the Q-loss
-    // columns' backward (dQ/da) and the actor chain only.  sX forks from sM and joins sM / sB;
-    // it never waits on sB or sF (capture rule above).
-    // (only with the Euler flow at 8 blocks per tile, i.e. <= 16 tiles: cube, 1-2 members; at
-    // 4 blocks per tile the 4th stream measured 12-14 % slower)
-    const bool small = h->opt.small_sched && h->sX != h->sM && h->stream_fwd && h->stream_bwd && h->fused_adam &&
-                       euler_split(h, c.nz) == 8;
+    // The 4th-stream schedule ("small-population schedule", since round 5
+    // at every population size): the target critic and, later, the critic's TD-column backward
+    // run on a 4th stream sX beside the main chain, which then carries the critic forward, the
+    // Q-loss columns' backward (dQ/da) and the actor chain only.  sX forks from sM and joins
+    // sM / sB; it never waits on sB or sF (capture rule above).  Same box against three
+    // streams: +3.7 % at 6 members, +3.3 % at 8, +0.9 % at 12, +1.6 / +2.1 % at ant 2 / 4,
+    // neutral at 4 and 16 (round 4's -12-14 % at 4 members was under the old split plan)
+    const bool small = h->opt.small_sched && h->sX != h->sM && h->stream_fwd && h->stream_bwd && h->fused_adam;
     {
         int plan[SITE_N];
         bool plan_small = false;

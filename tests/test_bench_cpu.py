@@ -211,14 +211,15 @@ def _plan(members, **cfg):
 
 def test_split_plan_per_members_and_workload():
     """The split plan chosen from same-box A/B runs (DESIGN.md section 6,
-    profiles/round5c): cube at 1-2 members splits every launch with the 4th stream; at 2 members
-    the critic's LN backward takes 4 blocks per tile (256 blocks, not 512); at 4 members the
-    Euler flow runs at 4 blocks per tile without the 4th stream (12-14 % faster than with it);
-    from 8 members nothing splits (the one-step backward at 128 tiles measured 2.4 % slower
-    split); the BC forward, target critic and critic forward run unsplit from 96 tiles (3-5 %
-    faster), the one-step forward (the chain's first launch) splits up to 128.  antsoccer
-    (B = 1024): one member splits the flow and the one-step backward, two members run
-    unsplit."""
+    profiles/round5c, round5e): cube at 1-2 members splits every launch; at 2 members the
+    critic's LN backward takes 4 blocks per tile (256 blocks, not 512); at 4 members the Euler
+    flow runs at 4 blocks per tile; from 6 members nothing splits (the one-step backward at
+    128 tiles measured 2.4 % slower split); the BC forward, target critic and critic forward
+    run unsplit from 96 tiles (3-5 % faster), the one-step forward (the chain's first launch)
+    splits up to 128.  antsoccer (B = 1024): one member splits the flow and the one-step
+    backward, two members run unsplit.  The 4th-stream schedule (target critic and TD-column
+    backward on sX) runs at every size since round 5 (+1-4 % at 6-12 members and ant 2-4,
+    neutral at 4 and 16: profiles/round5e/ab_small_sched_everywhere.txt)."""
     import fqlpop
     fqlpop.reset_engine_options()
     p = _plan(1)
@@ -230,17 +231,17 @@ def test_split_plan_per_members_and_workload():
     assert p["critic_forward"] == 1 and p["target_critic"] == 4 and p["onestep_backward"] == 8
     assert p["onestep_forward"] == 2 and p["bc_forward"] == 4
     p = _plan(4)
-    assert not p["small_sched"] and p["euler_flow"] == 4 and p["critic_backward_td"] == 1
+    assert p["small_sched"] and p["euler_flow"] == 4 and p["critic_backward_td"] == 1
     assert p["onestep_backward"] == 4 and p["critic_forward"] == 1 and p["critic_backward"] == 1
     assert p["bc_forward"] == 1 and p["target_critic"] == 1
-    for m in (8, 16):
+    for m in (6, 8, 16):
         p = _plan(m)
-        assert not p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES), (m, p)
+        assert p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES), (m, p)
     p = _plan(1, obs_dim=42, action_dim=8, batch_size=1024)
-    assert not p["small_sched"] and p["euler_flow"] == 4 and p["critic_backward_td"] == 1
+    assert p["small_sched"] and p["euler_flow"] == 4 and p["critic_backward_td"] == 1
     assert p["bc_forward"] == 1 and p["target_critic"] == 1 and p["onestep_backward"] == 4
     p = _plan(2, obs_dim=42, action_dim=8, batch_size=1024)
-    assert not p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES), p
+    assert p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES), p
 
 
 def test_split_plan_follows_engine_options():
@@ -248,13 +249,16 @@ def test_split_plan_follows_engine_options():
     try:
         fqlpop.set_engine_option("split", 0)
         p = _plan(1)
-        assert not p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES)
+        assert p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES)
         fqlpop.reset_engine_options()
-        fqlpop.set_engine_option("split_sites", 1 << 3)  # the Euler flow unsplit: no 4th stream
+        fqlpop.set_engine_option("split_sites", 1 << 3)  # the Euler flow unsplit
         p = _plan(2)
-        assert p["euler_flow"] == 1 and not p["small_sched"] and p["onestep_forward"] > 1
+        assert p["euler_flow"] == 1 and p["small_sched"] and p["onestep_forward"] > 1
         fqlpop.reset_engine_options()
-        fqlpop.set_engine_option("serial", 1)  # one stream: no small-population schedule
+        fqlpop.set_engine_option("small_sched", 0)  # three streams
+        assert not _plan(2)["small_sched"] and not _plan(16)["small_sched"]
+        fqlpop.reset_engine_options()
+        fqlpop.set_engine_option("serial", 1)  # one stream: no 4th-stream schedule
         assert not _plan(2)["small_sched"]
     finally:
         fqlpop.reset_engine_options()

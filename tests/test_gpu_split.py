@@ -72,13 +72,14 @@ def test_split_bit_identical_to_unsplit_cube(n, F):
     _same(got, ref)
 
 
-@pytest.mark.parametrize("n", [1, 2])
-def test_small_population_schedule_bit_identical(n):
-    """The small-population schedule (engine option small_sched: the target critic and the
-    critic's TD-column backward on a fourth stream, the Q-loss columns' backward as a launch
-    of its own) changes where launches run, not what they compute."""
-    ref = _run({"split": 8, "small_sched": 0}, n)
-    got = _run({"split": 8, "small_sched": 1}, n)
+@pytest.mark.parametrize("n,split", [(1, 8), (2, 8), (4, 1), (8, 1)])
+def test_small_population_schedule_bit_identical(n, split):
+    """The 4th-stream schedule (engine option small_sched, on at every population size since
+    round 5: the target critic and the critic's TD-column backward on a fourth stream, the
+    Q-loss columns' backward as a launch of its own) changes where launches run, not what
+    they compute: bit-identical to three streams, split (1-2 members) and unsplit (8)."""
+    ref = _run({"split": split, "small_sched": 0}, n)
+    got = _run({"split": split, "small_sched": 1}, n)
     _same(got, ref)
 
 
