@@ -569,6 +569,9 @@ void gemm(int layout, int epi, const GemmArgs& g, hipStream_t s) {
 // critic, critic forwards, critic and one-step backwards (sM); in the 4th-stream schedule
 // the target critic and the critic's TD-column backward (SITE_CRB2) run on sX.  The
 // BC backward (sB) stays unsplit.
+// the 4th-stream schedule runs up to this many 16-column tiles per step (B / 16 x members):
+// cube 16 members (256) neutral, ant 4 (256) +2.1 %, ant 16 (1 024) -1.1 %
+constexpr long long kSmallSchedTiles = 256;
 enum { SITE_BCF = 0, SITE_EULER = 1, SITE_OSF = 2, SITE_TGT = 3, SITE_CRF = 4, SITE_CRB = 5, SITE_OSB = 6, SITE_CRB2 = 7,
        SITE_N = 8 };
 // a site with more 16-column tiles than its cap runs unsplit (same-box A/B, DESIGN.md section 5,
@@ -633,7 +636,8 @@ void split_plan(const EngineOptions& o, const SplitShape& d, int nz, int F[SITE_
     };
     fwd(SITE_EULER, d.K0bc, d.A, B, (long long)T * nz, true);
     if (!d.euler_fused) F[SITE_EULER] = 1;
-    *small = o.small_sched && d.multi_stream && d.stream_fwd && d.stream_bwd && d.fused_adam;
+    *small = o.small_sched && d.multi_stream && d.stream_fwd && d.stream_bwd && d.fused_adam &&
+             (long long)T * nz <= kSmallSchedTiles;
     fwd(SITE_BCF, d.K0bc, d.A, B2, (long long)(B2 / 16) * nz, false);
     fwd(SITE_OSF, d.K0os, d.A, B3, (long long)(B3 / 16) * nz, false);
     fwd(SITE_TGT, d.K0cr, 1, B, (long long)T * d.E * nz, false);
@@ -1438,8 +1442,10 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     // Q-loss columns' backward (dQ/da) and the actor chain only.  sX forks from sM and joins
     // sM / sB; it never waits on sB or sF (capture rule above).  Same box against three
     // streams: +3.7 % at 6 members, +3.3 % at 8, +0.9 % at 12, +1.6 / +2.1 % at ant 2 / 4,
-    // neutral at 4 and 16 (round 4's -12-14 % at 4 members was under the old split plan)
-    const bool small = h->opt.small_sched && h->sX != h->sM && h->stream_fwd && h->stream_bwd && h->fused_adam;
+    // neutral at 4 and 16 (round 4's -12-14 % at 4 members was under the old split plan),
+    // -1.1 % at ant 16 (1 024 tiles): on up to kSmallSchedTiles 16-column tiles
+    const bool small = h->opt.small_sched && h->sX != h->sM && h->stream_fwd && h->stream_bwd && h->fused_adam &&
+                       (long long)(h->B / 16) * c.nz <= kSmallSchedTiles;
     {
         int plan[SITE_N];
         bool plan_small = false;

@@ -218,8 +218,9 @@ def test_split_plan_per_members_and_workload():
     run unsplit from 96 tiles (3-5 % faster), the one-step forward (the chain's first launch)
     splits up to 128.  antsoccer (B = 1024): one member splits the flow and the one-step
     backward, two members run unsplit.  The 4th-stream schedule (target critic and TD-column
-    backward on sX) runs at every size since round 5 (+1-4 % at 6-12 members and ant 2-4,
-    neutral at 4 and 16: profiles/round5e/ab_small_sched_everywhere.txt)."""
+    backward on sX) runs up to 256 tiles per step since round 5 (+1-4 % at 6-12 members and
+    ant 2-4, neutral at 4 and 16, -1.1 % at ant 16: profiles/round5e/ab_small_sched_everywhere.txt,
+    ab_4th_stream_ant16_cube3.txt)."""
     import fqlpop
     fqlpop.reset_engine_options()
     p = _plan(1)
@@ -242,6 +243,10 @@ def test_split_plan_per_members_and_workload():
     assert p["bc_forward"] == 1 and p["target_critic"] == 1 and p["onestep_backward"] == 4
     p = _plan(2, obs_dim=42, action_dim=8, batch_size=1024)
     assert p["small_sched"] and all(p[s] == 1 for s in fqlpop.population.SPLIT_SITES), p
+    # the 4th stream up to 256 tiles per step (cube 16 members: neutral; ant 16: -1.1 %)
+    assert not _plan(16, obs_dim=42, action_dim=8, batch_size=1024)["small_sched"]
+    assert not _plan(8, obs_dim=42, action_dim=8, batch_size=1024)["small_sched"]
+    assert not _plan(17)["small_sched"]
 
 
 def test_split_plan_follows_engine_options():
