@@ -82,8 +82,10 @@ const char* fqlpop_last_error(void);
  *   split (0 off, 1 auto, 2 / 4 / 8: small populations run the streamed forwards, the
  *   Euler flow and the critic / one-step backwards as clusters of 2-8 blocks per 16-column
  *   tile; bit-identical to the unsplit kernels),
- *   small_sched (0/1: with the Euler flow split, the target critic and the critic's
- *   TD-column backward run on a fourth stream),
+ *   small_sched (0/1: up to 256 16-column tiles per step, the target critic and the
+ *   critic's TD-column backward run on a fourth stream; bit-identical),
+ *   split_sites, split_blocks (per-site split factors and the block cap of a split forward,
+ *   for A/B runs),
  *   hw_queues (1..1024, default 4): the GPU_MAX_HW_QUEUES the caller runs the HIP runtime
  *   with.  Below 4 the step is captured on one stream: ROCm 7's graph launch can index past
  *   its pool of branch streams when more than one shares the launch stream's hardware queue.
@@ -99,9 +101,9 @@ int fqlpop_reset_engine_options(void);
 /* The split plan a population of n_members created now with `cfg` would run (no GPU call):
  * blocks per 16-column tile of each split launch site, 1 = the unsplit kernel, in site order
  * {BC forward, Euler flow, one-step forward, target critic, critic forward, critic backward
- * (its Q-loss columns under the small-population schedule), one-step backward, critic
- * TD-column backward (small-population schedule only)} (blocks_per_tile[8]), and whether the
- * small-population schedule (4th stream) runs.  The step checks each launch against this plan.
+ * (its Q-loss columns under the 4th-stream schedule), one-step backward, critic
+ * TD-column backward (4th-stream schedule only)} (blocks_per_tile[8]), and whether the
+ * 4th-stream schedule runs.  The step checks each launch against this plan.
  * [no reference counterpart: engine introspection] */
 int fqlpop_split_plan(const fqlpop_config* cfg, int n_members, int* blocks_per_tile, int* small_sched);
 /* Streams (parallel graph branches) a population created now would capture its step on:
