@@ -209,8 +209,12 @@ struct SplitFwdArgs {
     unsigned long long* probe;   // optional per-block {start, end} stamps
     SplitSync sync;
     unsigned long long* phase;   // diagnostics (FQLPOP_PHASE_PROBE, Euler): [EF_PHASE_STRIDE] per block
+    float* pre0;                 // Euler: layer-0 accumulators, split_euler_pre0_floats() per block
 };
 long long split_cluster_bytes();
+constexpr long long split_euler_pre0_floats() { return 2LL * 256 * 16; }  // [h][thread][16]
+// the Euler flow's layer-0 form: its observation rows once per launch (split_fwd_kernel PRE0)
+bool split_euler_pre0(int K0, int D);
 int split_counter_stride();
 bool split_fwd_supported(int H, int L, int K0, int nout, int M);
 // F = 8, 4 or 2 blocks per 16-column tile; grid = tiles x ny x nz x F blocks of 256 threads

@@ -1847,7 +1847,16 @@ bool split_fwd_supported(int H, int L, int K0, int nout, int M) {
     return H == EF_H && L >= 3 && L <= EF_MAX_LAYERS && K0 <= EF_K0MAX && nout <= 8 && M % EF_NC == 0;
 }
 
-template <int MODE, bool LN, bool EULER, int TPW>
+// The Euler flow's layer-0 form (split_fwd_kernel's PRE0): the observation rows' k-steps
+// once per launch, at most 2 k-steps of its own per flow step (see pre0g in the kernel)
+constexpr int sp_ns0(int K0, bool tail0) { return tail0 ? EF_PF : (K0 + 4 * EF_PF - 1) / (4 * EF_PF) * EF_PF; }
+bool split_euler_pre0(int K0, int D) {
+    const bool tail0 = K0 > 4 * EF_PF && K0 <= 4 * (EF_PF + 1);
+    const int npre = D / 4, nps = sp_ns0(K0, tail0) + (tail0 ? 1 : 0) - npre;
+    return npre > 0 && nps >= 1 && nps <= 2;
+}
+
+template <int MODE, bool LN, bool EULER, int TPW, bool PRE0 = false>
 __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs a) {
     constexpr int H = EF_H, NC = EF_NC, NT = SP_NT, PF = EF_PF, F = 8 / TPW, FB = H / F;
     const StreamArgs& g = a.s;
@@ -1891,7 +1900,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
     auto stamp = [](int, int, int) {};
 #endif
     const bool tail0 = K0 > 4 * PF && K0 <= 4 * (PF + 1);
-    const int NS0 = tail0 ? PF : (K0 + 4 * PF - 1) / (4 * PF) * PF;
+    const int NS0 = sp_ns0(K0, tail0);
     const float* __restrict__ P = g.params + (long long)slot * g.P + (long long)y * g.ens;
     const rsrc_t rW = make_rsrc(P, g.P);
     unsigned long long* const X = a.sync.xch + (long long)cl * SP_CLUSTER_GRANULES;
@@ -1902,6 +1911,72 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
     load_in0<NT>(in0, g.x0 + (long long)slot * g.x0_ss, K0, g.ld_x, c0);
     __syncthreads();
     stamp(-1, 0, 1);
+
+    // Euler flow, layer 0 (computed in every block, all 512 features): its observation rows
+    // are the same at every flow step, so the first NPRE k-steps of each feature's chain
+    // (rows < 4 NPRE <= D) run once per launch, and every step resumes the chain from their
+    // accumulators with its own k-steps (action and time rows, then the zero rows up to the
+    // unsplit kernel's k-step count, tail included): the same MFMAs in the same order as
+    // the full chain, bit-identical.  The accumulators (32 per thread) live in a global
+    // scratch slab of the block's ticket (a.pre0; each thread reads back only its own
+    // words): 32 KB of LDS per block would cost the kernels beside the flow their
+    // co-residency.  A step's own A fragments are loaded before the
+    // previous step's head wait, the accumulators at the start of its layer 0.  Taken when a step has at most 2
+    // k-steps of its own (cube: 7 of 9 k-steps once per launch).
+    const int NPRE = EULER ? a.D / 4 : 0, NPS = NS0 + (tail0 ? 1 : 0) - NPRE;
+    constexpr bool fast0 = EULER && PRE0;  // the host checked split_euler_pre0(K0, D)
+    float4 a0[2][2], pv[2][4];
+    float* const pre0g = fast0 ? a.pre0 + ((long long)ticket * 2 * NT + tid) * 16 : nullptr;  // [h] at + h NT 16
+    auto load_step0 = [&]() {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int lo0 = lk * H + 64 * (2 * q + h) + 4 * li;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                a0[h][j] = j < NPS ? bload4(rW, (int)g.w_off[0] + 4 * (NPRE + j) * H + lo0) : float4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto load_pv = [&]() {  // the accumulators: at layer 0 (across the head wait they would spill)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) pv[h][c] = *reinterpret_cast<const float4*>(pre0g + (long long)h * NT * 16 + 4 * c);
+    };
+    if constexpr (fast0) {
+        // both unsplit waves' loads of a batch of 8 k-steps in flight together
+        f32x4 acc[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s0 = 0; s0 < NPRE; s0 += 8) {
+            float4 t[2][8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    t[h][j] = s0 + j < NPRE ? bload4(rW, (int)g.w_off[0] + 4 * (s0 + j) * H + lk * H + 64 * (2 * q + h) + 4 * li)
+                                            : float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (s0 + j < NPRE) {
+                        const float b = in0[(4 * (s0 + j) + lk) * NC + li];
+                        acc[h][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(t[h][j].x, b, acc[h][0], 0, 0, 0);
+                        acc[h][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(t[h][j].y, b, acc[h][1], 0, 0, 0);
+                        acc[h][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(t[h][j].z, b, acc[h][2], 0, 0, 0);
+                        acc[h][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(t[h][j].w, b, acc[h][3], 0, 0, 0);
+                    }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                *reinterpret_cast<float4*>(pre0g + (long long)h * NT * 16 + 4 * c) =
+                    float4{acc[h][c][0], acc[h][c][1], acc[h][c][2], acc[h][c][3]};
+        load_step0();
+    }
 
     // LayerNorm statistics of one column from the 8 unsplit-wave partials (stream_fwd_kernel's sums)
     auto col_stats = [&](int col, float& mean, float& rs) {
@@ -1971,25 +2046,47 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
         (void)pst;
         // ---- layer 0, redundantly in every block: unsplit waves 2q, 2q + 1 ----
         stamp(pst, 0, 0);
+        if constexpr (fast0) load_pv();
         stamp(pst, 0, 1);
         {
             float v[2][4][4];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int w = 2 * q + h;
-                const int lo = lk * H + 64 * w + 4 * li;
-                float4 ring[PF];
-#pragma unroll
-                for (int p = 0; p < PF; ++p) ring[p] = bload4(rW, (int)g.w_off[0] + 4 * p * H + lo);
-                const float4 at0 = bload4(rW, (int)g.w_off[0] + 4 * PF * H + lo);
                 float4 bias4[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) bias4[r] = bload4(rW, (int)g.b_off[0] + 64 * w + 16 * lk + 4 * r);
                 f32x4 acc[4];
+                bool done0 = false;
+                if constexpr (EULER) {
+                    if constexpr (fast0) {  // resume the chain after the observation rows (see pre0g)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-                ef_kloop(acc, ring, rW, in0, NS0, (int)g.w_off[0], (int)g.w_off[0], lo, lk, li);
-                if (tail0) ef_tail(acc, at0, in0, lk, li);
+                        for (int r = 0; r < 4; ++r) bias4[r] = bload4(rW, (int)g.b_off[0] + 64 * w + 16 * lk + 4 * r);
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) acc[c] = f32x4{pv[h][c].x, pv[h][c].y, pv[h][c].z, pv[h][c].w};
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            if (j < NPS) {
+                                const float b = in0[(4 * (NPRE + j) + lk) * NC + li];
+                                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[h][j].x, b, acc[0], 0, 0, 0);
+                                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[h][j].y, b, acc[1], 0, 0, 0);
+                                acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[h][j].z, b, acc[2], 0, 0, 0);
+                                acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[h][j].w, b, acc[3], 0, 0, 0);
+                            }
+                        done0 = true;
+                    }
+                }
+                if (!done0) {
+                    const int lo = lk * H + 64 * w + 4 * li;
+                    float4 ring[PF];
+#pragma unroll
+                    for (int p = 0; p < PF; ++p) ring[p] = bload4(rW, (int)g.w_off[0] + 4 * p * H + lo);
+                    const float4 at0 = bload4(rW, (int)g.w_off[0] + 4 * PF * H + lo);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) bias4[r] = bload4(rW, (int)g.b_off[0] + 64 * w + 16 * lk + 4 * r);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    ef_kloop(acc, ring, rW, in0, NS0, (int)g.w_off[0], (int)g.w_off[0], lo, lk, li);
+                    if (tail0) ef_tail(acc, at0, in0, lk, li);
+                }
                 const bool stU = st && g.U[0] && 64 * w >= fb && 64 * w < fb + FB;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -2182,6 +2279,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
             // every block: the 8 unsplit-wave head partials, summed in euler_flow_kernel's order
             const unsigned tag = sp_tag(gen, phase - 1);
             stamp(pst, L, 0);
+            if (fast0 && step + 1 < a.S) load_step0();  // the next step's layer-0 operands, during the wait
             if (tid < a.A * NC) {
                 const int aa = tid / NC, j = tid % NC;
                 float v = gx_get(X, SP_G_HP + aa * NC + j, tag, a.sync);
@@ -2211,6 +2309,7 @@ __global__ __launch_bounds__(SP_NT, 2) void split_fwd_kernel(const SplitFwdArgs 
 void launch_split_fwd(int head_mode, bool ln, bool euler, int F, const SplitFwdArgs& a, hipStream_t s) {
     const dim3 grid((a.s.M / EF_NC) * a.s.ny * a.s.nz * F), block(SP_NT);
 #define FQ_SPF(MODE, LNV, EU, T) hipLaunchKernelGGL((split_fwd_kernel<MODE, LNV, EU, T>), grid, block, 0, s, a)
+#define FQ_SPF0(T) hipLaunchKernelGGL((split_fwd_kernel<HEAD_EULER, false, true, T, true>), grid, block, 0, s, a)
 #define FQ_SPF_T(MODE, LNV, EU)                          \
     switch (F) {                                         \
         case 8: FQ_SPF(MODE, LNV, EU, 1); break;         \
@@ -2218,8 +2317,12 @@ void launch_split_fwd(int head_mode, bool ln, bool euler, int F, const SplitFwdA
         default: FQ_SPF(MODE, LNV, EU, 4); break;        \
     }
     if (euler) {
-        if (F == 8) FQ_SPF(HEAD_EULER, false, true, 1);
-        else FQ_SPF(HEAD_EULER, false, true, 2);
+        const bool pre0 = a.pre0 != nullptr && split_euler_pre0(a.s.K0, a.D);
+        if (F == 8) {
+            if (pre0) FQ_SPF0(1); else FQ_SPF(HEAD_EULER, false, true, 1);
+        } else {
+            if (pre0) FQ_SPF0(2); else FQ_SPF(HEAD_EULER, false, true, 2);
+        }
     } else {
         switch (head_mode) {
             // (the actors have no LayerNorm: actor_layer_norm is refused at create)
@@ -2229,6 +2332,7 @@ void launch_split_fwd(int head_mode, bool ln, bool euler, int F, const SplitFwdA
         }
     }
 #undef FQ_SPF_T
+#undef FQ_SPF0
 #undef FQ_SPF
 }
 

@@ -282,6 +282,8 @@ struct fqlpop {
     } split_site[8];
     unsigned* split_err = nullptr;       // device pointer of split_err_host (mapped, coherent host memory)
     unsigned* split_err_host = nullptr;  // the host reads it without a copy or a synchronisation
+    float* euler_pre0 = nullptr;         // the split Euler flow's layer-0 accumulators (SplitFwdArgs::pre0)
+    long long euler_pre0_blocks = 0;     // its capacity in blocks
     bool split_ok = false;
     bool stream_fwd = false;       // whole-network forward launches (stream_fwd_kernel)
     bool stream_bwd = false;       // whole-network dX chains (stream_bwd_kernel)
@@ -1094,6 +1096,9 @@ SplitFwdArgs euler_split_args(fqlpop* h, const EulerArgs& ea, hipStream_t s) {
     sa.probe = ea.probe;
     sa.phase = ea.phase;
     sa.sync = split_prep(h, SITE_EULER, (long long)(ea.B / 16) * ea.nz, s);
+    // the layer-0 scratch when it covers the launch (else the kernel's full layer-0 chain)
+    const long long blocks = (long long)(ea.B / 16) * ea.nz * euler_split(h, ea.nz);
+    sa.pre0 = h->euler_pre0 && blocks <= h->euler_pre0_blocks ? h->euler_pre0 : nullptr;
     return sa;
 }
 long long euler_blocks(const fqlpop* h, int nz) { return (long long)(h->B / 16) * nz * euler_split(h, nz); }
@@ -2015,6 +2020,12 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
                 HIPCHK(hipMalloc(&st.gen, 64));
                 HIPCHK(hipMemset(st.gen, 0, 64));
             }
+            // the split Euler flow's layer-0 accumulators: 32 KB per block, for the largest split
+            // Euler launch (up to 128 tiles at 8 blocks each)
+            if (split_euler_pre0(D + A + 1, D)) {
+                h->euler_pre0_blocks = std::min<long long>(h->split_site[SITE_EULER].clusters, 128) * 8;
+                HIPCHK(hipMalloc(&h->euler_pre0, sizeof(float) * split_euler_pre0_floats() * h->euler_pre0_blocks));
+            }
             // the error word lives in host memory so that every entry point can test it without a
             // device-to-host copy (fqlpop_step does, before it enqueues more steps)
             HIPCHK(hipHostMalloc((void**)&h->split_err_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -2075,6 +2086,7 @@ int fqlpop_destroy(fqlpop_t* h) {
             if (st.cnt) (void)hipFree(st.cnt);
             if (st.gen) (void)hipFree(st.gen);
         }
+        if (h->euler_pre0) (void)hipFree(h->euler_pre0);
         if (h->split_err_host) (void)hipHostFree(h->split_err_host);
         for (hipEvent_t e : {h->ev_sample, h->ev_bcfwd, h->ev_bcloss, h->ev_flow, h->ev_bdone, h->ev_t0, h->ev_t1})
             if (e) (void)hipEventDestroy(e);
