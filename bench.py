@@ -180,17 +180,14 @@ def _cgroup_cpu_quota():
 
 
 def cpu_allotment() -> dict:
-    """The CPUs this process may actually keep busy: the smallest of sched_getaffinity, the
-    cgroup quota and OMP_NUM_THREADS (the box exports the job's CPU share there; its
-    affinity mask and os.cpu_count() show the whole 256-CPU host)."""
+    """The CPUs this process may actually keep busy: the smaller of sched_getaffinity and the
+    cgroup CPU quota (the box's affinity mask and os.cpu_count() show the whole 256-CPU host;
+    its cgroup quota is the job's share).  OMP_NUM_THREADS is recorded but does not cap the
+    count: a launcher that exports OMP_NUM_THREADS=1 must not turn the CPU leg single-threaded
+     while the host grants more CPUs."""
     host = host_cpu()
     quota = _cgroup_cpu_quota()
-    omp = host["omp_num_threads"]
-    try:
-        omp = int(omp) if omp else None
-    except ValueError:
-        omp = None
-    cands = [c for c in (host["affinity_cpus"], quota, omp) if c]
+    cands = [c for c in (host["affinity_cpus"], quota) if c]
     host["cgroup_quota_cpus"] = quota
     host["effective_cpus"] = max(1, min(cands) if cands else (os.cpu_count() or 1))
     return host
@@ -241,10 +238,10 @@ def cpu_baseline(wl: dict, data: dict, budget_s: float, thread_counts=None) -> d
                       f"{r['elapsed']:.1f} s after a {r['warmup_s']:.2f} s warm-up update, float32 PyTorch-CPU "
                       f"restatement (oracle/fql_torch.py), torch threads={best}: the best of "
                       f"{', '.join(str(t) for t in counts)} thread(s), {share:.1f} s wall budget each "
-                      f"(effective CPUs {eff} = min of sched_getaffinity {host['affinity_cpus']}, cgroup quota "
-                      f"{host['cgroup_quota_cpus']}, OMP_NUM_THREADS {host['omp_num_threads']}; os.cpu_count() "
-                      f"{host['os_cpu_count']}). BASELINE C1 (1k steps) extrapolated from this rate: "
-                      f"{1000.0 / r['rate']:.0f} s"}
+                      f"(effective CPUs {eff} = min of sched_getaffinity {host['affinity_cpus']} and cgroup quota "
+                      f"{host['cgroup_quota_cpus']}; OMP_NUM_THREADS {host['omp_num_threads']} recorded, not a cap; "
+                      f"os.cpu_count() {host['os_cpu_count']}). BASELINE C1 (1k steps) is timed, not extrapolated, "
+                      f"by bench.py --c1 (profiles/round6*/c1_cpu_1k_steps.json)"}
 
 
 def _cpu_rate(wl: dict, data: dict, budget_s: float, threads: int) -> dict:
@@ -288,6 +285,52 @@ def _cpu_rate(wl: dict, data: dict, budget_s: float, threads: int) -> dict:
             break
     return {"rate": steps / el, "steps": steps, "elapsed": el, "warmup_s": warm, "longest_update_s": longest,
             "note": None}
+
+
+def c1_cpu_run(steps: int, rows: int) -> dict:
+    """BASELINE config 1 timed, not extrapolated: cube-single shapes, one
+    member at alpha = 10, B = 256, H = 512 x 4, `steps` sequential update() calls on the host
+    CPU only (no GPU call).  The reference runs this on CPU JAX, which is absent here; the
+    float32 PyTorch restatement of the same update (oracle/fql_torch.py, kind "port") runs at
+    the effective CPU allotment (cpu_allotment).  Minibatches are drawn from the synthetic
+    1M-row buffer on the host, as the reference's task.sample does, inside the timed loop."""
+    from oracle import fql_oracle as O
+    from oracle.fql_torch import TorchFQL
+    wl = WORKLOADS["cube"]
+    host = cpu_allotment()
+    threads = host["effective_cpus"]
+    torch.set_num_threads(threads)
+    data = synthetic_dataset(rows, wl["obs_dim"], wl["action_dim"])
+    cfg = O.OracleConfig(obs_dim=wl["obs_dim"], action_dim=wl["action_dim"], batch_size=wl["batch_size"],
+                         alpha=10.0)
+    agent = TorchFQL(cfg, O.cast_tree(O.init_params(cfg, 0), np.float32))
+    rng = np.random.default_rng(1)
+    B, A, N = cfg.batch_size, cfg.action_dim, data["observations"].shape[0]
+
+    def draw():
+        idx = rng.integers(0, N, B)
+        b = {k: torch.from_numpy(np.ascontiguousarray(v[idx])) for k, v in data.items()}
+        nz = {"z_next": torch.randn(B, A), "x0": torch.randn(B, A), "t": torch.rand(B, 1),
+              "z_d": torch.randn(B, A), "z_metric": torch.randn(B, A)}
+        return b, nz
+
+    t_w = time.perf_counter()
+    agent.update(*draw())  # first call: allocator and thread-pool warm-up, not timed
+    warm = time.perf_counter() - t_w
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(steps):
+        last = agent.update(*draw())
+    wall = time.perf_counter() - t0
+    info = {k: float(v) for k, v in (last or {}).items()} if isinstance(last, dict) else {}
+    return {"metric": f"BASELINE C1: wall time of {steps} FQL update() steps on the host CPU (no GPU)",
+            "value": round(wall, 3), "unit": "s", "steps": steps, "higher_is_better": False,
+            "member_grad_steps_per_s": round(steps / wall, 3), "threads": threads, "warmup_update_s": round(warm, 3),
+            "kind": "port", "host": host, "dtype": "f32",
+            "config": {"workload": f"{wl['env']} single alpha=10 update(), B={B}, H=512x4, obs {wl['obs_dim']}, "
+                                   f"act {wl['action_dim']}, flow_steps 10", "rows": rows},
+            "data": "synthetic (seeded numpy), host-sampled minibatches inside the timed loop",
+            "finite": bool(all(np.isfinite(v) for v in info.values())) if info else None}
 
 
 def eval_rollout_leg(pop, wl: dict, n_envs: int, steps: int, dev) -> dict:
@@ -415,6 +458,10 @@ def main(argv=None):
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_dominant.json"),
                     help="HBM bytes per dominant-kernel launch measured by rocprofv3 --pmc passes "
                          "(csrc/tools/pmc_summary.py output); missing file -> traffic null")
+    ap.add_argument("--kernel-times-json", default=os.path.join(ROOT, "profiles", "kernel_times.json"),
+                    help="per-kernel in-step and serial launch times of the 16-member step (rocprofv3 stats, "
+                         "csrc/tools/kernel_times.py output): the roofline's serial fraction and the in-step "
+                         "top kernel; missing file -> those fields null")
     ap.add_argument("--preheat-ms", type=float, default=300.0,
                     help="replays of the dominant kernel alone before the warmup steps (GPU clock ramp); 0 = off")
     ap.add_argument("--preheat-kind", choices=("steps", "kernel"), default="steps",
@@ -434,6 +481,9 @@ def main(argv=None):
     ap.add_argument("--engine-option", action="append", default=[], metavar="NAME=VALUE",
                     help="fqlpop_set_engine_option before the population is created (alternate schedules / "
                          "code paths with the same results; recorded in the JSON line)")
+    ap.add_argument("--c1", action="store_true",
+                    help="BASELINE config 1 only: --steps (default 1000 here) update() steps of one member on the "
+                         "host CPU (no GPU call); prints its own JSON line")
     ap.add_argument("--diagnostic", action="store_true",
                     help="allow FQLPOP_* environment variables (developer A/B runs); they are recorded")
     args = ap.parse_args(argv)
@@ -445,6 +495,10 @@ def main(argv=None):
         log(f"bench.py: refusing to measure with {sorted(fq_env)} set (developer switches); "
             "unset them or pass --diagnostic")
         return 2
+    if args.c1:
+        steps = args.steps if "--steps" in (sys.argv[1:] if argv is None else list(argv)) else 1000
+        print(json.dumps(c1_cpu_run(steps, args.rows)), flush=True)
+        return 0
     if args.gpus < 1:
         log("bench.py: --gpus must be >= 1")
         return 2
@@ -596,6 +650,28 @@ def main(argv=None):
             traffic_src = {"file": os.path.relpath(args.pmc_json, ROOT), "commit": pmc.get("commit"),
                            "date": pmc.get("date")}
 
+    # the roofline's other views of the same kernel: alone (live replays
+    # above), serial-stream launch and in-step top kernel by time (rocprofv3, kernel_times.json)
+    serial_view, top_view = None, None
+    if os.path.exists(args.kernel_times_json):
+        with open(args.kernel_times_json) as f:
+            kt = json.load(f)
+        if kt.get("members") == pop.n and kt.get("workload", "cube") == args.workload:
+            src = {"file": os.path.relpath(args.kernel_times_json, ROOT), "commit": kt.get("commit"),
+                   "instep_source": kt.get("instep_source"), "serial_source": kt.get("serial_source")}
+            kd = kt["kernels"].get(kname.split("(")[0])
+            if kd and kd.get("serial_avg_us"):
+                serial_view = {"serial_launch_us": kd["serial_avg_us"],
+                               "frac": round(kflops / (kd["serial_avg_us"] * 1e-6) / 1e12 / MI355X_FP32_MFMA_PEAK_TFLOPS, 4),
+                               "rocprof_in_step_launch_us": kd["in_step_avg_us"], "source": src}
+            top_name = next(iter(kt["kernels"]))
+            td = kt["kernels"][top_name]
+            top_view = {"kernel": top_name, "launches_per_step": td["launches_per_step"],
+                        "in_step_us_per_step": td["in_step_us_per_step"],
+                        "serial_us_per_step": td.get("serial_us_per_step"), "stretch": td.get("stretch"),
+                        "source": src}
+    step_frac = flops_ms * value / 1e12 / (MI355X_FP32_MFMA_PEAK_TFLOPS * world)
+
     result = {
         # BASELINE.json's metric: the whole population (16 members by default) over all ranks
         "metric": f"FQL grad-steps/sec (whole node) over {n_total}-α population, "
@@ -645,6 +721,15 @@ def main(argv=None):
             "peak": MI355X_FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / MI355X_FP32_MFMA_PEAK_TFLOPS, 4),
+            "frac_in_step": round(achieved / MI355X_FP32_MFMA_PEAK_TFLOPS, 4),
+            "frac_isolated": round(kflops / (iso_us * 1e-6) / 1e12 / MI355X_FP32_MFMA_PEAK_TFLOPS, 4),
+            "frac_serial_stream": serial_view,
+            "step_frac": round(step_frac, 4),
+            "in_step_top_kernel": top_view,
+            "fractions": "frac = frac_in_step: the dominant kernel's in-step launches (this run's stamps), "
+                         "sharing the CUs with the other streams; frac_isolated: the same launch replayed alone "
+                         "(this run); frac_serial_stream: its launch in a serial-stream step (rocprofv3, "
+                         "kernel_times.json); step_frac: the whole step's flops / wall time / peak",
             "avg_launch_us": round(launch_us, 3),
             "launches_timed": probe_n,
             "isolated_launch_us": round(iso_us, 3),

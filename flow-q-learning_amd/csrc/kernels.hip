@@ -25,6 +25,13 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+// The explicit waits (__builtin_amdgcn_s_waitcnt with vmcnt / lgkmcnt immediates, e.g. 0x0F74)
+// use the gfx9 simm16 field layout, which gfx10+ encodes differently; the v_permlane*_swap
+// inline asm exists on gfx950 only.  Device code is built for gfx950 alone (Makefile ARCH).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "fqlpop kernels target gfx950 (MI355X) only: the s_waitcnt immediates use the gfx9 encoding"
+#endif
+
 
 namespace fq {
 

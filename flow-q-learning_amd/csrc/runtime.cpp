@@ -282,7 +282,11 @@ struct fqlpop {
     } split_site[8];
     unsigned* split_err = nullptr;       // device pointer of split_err_host (mapped, coherent host memory)
     unsigned* split_err_host = nullptr;  // the host reads it without a copy or a synchronisation
-    float* euler_pre0 = nullptr;         // the split Euler flow's layer-0 accumulators (SplitFwdArgs::pre0)
+    // members whose state a failed split launch may have written (sticky until restored): bit
+    // w of restored[i] is set by fqlpop_set_state(i, w); all three restore the member, and so
+    // does fqlpop_set_member(i, ..., reinit = 1)
+    std::vector<unsigned char> poisoned, restored;
+    float* euler_pre0 = nullptr;        // the split Euler flow's layer-0 accumulators (SplitFwdArgs::pre0)
     long long euler_pre0_blocks = 0;     // its capacity in blocks
     bool split_ok = false;
     bool stream_fwd = false;       // whole-network forward launches (stream_fwd_kernel)
@@ -1747,16 +1751,43 @@ bool split_error_pending(const fqlpop* h) {
     return h->split_err_host && __atomic_load_n(h->split_err_host, __ATOMIC_ACQUIRE) != 0;
 }
 
-// A split launch whose hand-off wait gave up (kernels.hip, sp_fail) left invalid results:
-// report it (once) instead of returning them.  The caller has synchronised the streams.
-void check_split_error(fqlpop* h) {
-    if (split_error_pending(h)) {
-        __atomic_store_n(h->split_err_host, 0u, __ATOMIC_RELEASE);
-        for (auto& st : h->split_site)  // a launch that gave up may have left its counters set
-            if (st.cnt) HIPCHK(hipMemset(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (st.clusters + 2)));
-        throw FqErr{FQLPOP_E_STATE, "a split launch's hand-off wait timed out (blocks of a cluster not resident "
-                                    "together); results of the last steps are invalid"};
-    }
+// A split launch whose hand-off wait gave up (kernels.hip, sp_fail) left invalid results.
+// The failure is sticky per member: every member that was active poisons, and each entry
+// point that would train on or export a poisoned member's state keeps refusing until the
+// caller restores it (set_state of params, Adam m and Adam v, or set_member with reinit).
+// member < 0: any poisoned member refuses (whole-population calls).  The caller has
+// synchronised the streams.
+// The pending error word, if set, becomes the poison flags of the active members (returns true).
+bool absorb_split_error(fqlpop* h) {
+    if (!split_error_pending(h)) return false;
+    __atomic_store_n(h->split_err_host, 0u, __ATOMIC_RELEASE);
+    for (auto& st : h->split_site)  // a launch that gave up may have left its counters set
+        if (st.cnt) HIPCHK(hipMemset(st.cnt, 0, sizeof(unsigned) * split_counter_stride() * (st.clusters + 2)));
+    for (int i = 0; i < h->n; ++i)
+        if (h->active[i]) {
+            h->poisoned[i] = 1;
+            h->restored[i] = 0;
+        }
+    return true;
+}
+const char* const kSplitFailMsg =
+    "a split launch's hand-off wait timed out (blocks of a cluster not resident together); the state of every "
+    "member it stepped is invalid until restored (fqlpop_set_state of params, Adam m and v, or fqlpop_set_member "
+    "with reinit)";
+// only_active: whole-population training calls refuse for poisoned ACTIVE members only (a
+// pruned member does not step)
+void check_split_error(fqlpop* h, int member = -1, bool only_active = false) {
+    if (absorb_split_error(h)) throw FqErr{FQLPOP_E_STATE, kSplitFailMsg};
+    for (int i = member < 0 ? 0 : member; i < (member < 0 ? h->n : member + 1); ++i)
+        if (h->poisoned[i] && (!only_active || h->active[i]))
+            throw FqErr{FQLPOP_E_STATE, "member " + std::to_string(i) + "'s state was written by a failed split "
+                                        "launch; restore it first (fqlpop_set_state of params, Adam m and v, or "
+                                        "fqlpop_set_member with reinit)"};
+}
+void note_restored(fqlpop* h, int member, int which) {
+    if (!h->poisoned[member]) return;
+    h->restored[member] |= (unsigned char)(1u << which);
+    if (h->restored[member] == 7) h->poisoned[member] = 0;
 }
 
 void check_member(fqlpop* h, int member) {
@@ -2059,6 +2090,8 @@ int fqlpop_create(const fqlpop_config* cfg, int n_members, const float* alphas, 
         for (int i = 0; i < n; ++i) upload_skey(h.get(), i);
         for (int i = 0; i < n; ++i) init_member(h.get(), i, seeds_in[i]);
         h->active.assign(n, 1);
+        h->poisoned.assign(n, 0);
+        h->restored.assign(n, 0);
         update_slots(h.get());
         HIPCHK(hipDeviceSynchronize());
         *out = h.release();
@@ -2169,10 +2202,8 @@ int fqlpop_step(fqlpop_t* h, int n_steps) {
     return guard([&] {
         ARGCHK(h, "null handle");
         ARGCHK(n_steps >= 0, "n_steps must be >= 0");
-        if (split_error_pending(h)) {  // a stale error stops training (no copy, no sync when clear)
-            sync_all_streams(h);
-            check_split_error(h);
-        }
+        if (split_error_pending(h)) sync_all_streams(h);  // (no copy, no sync when clear)
+        check_split_error(h, -1, true);  // a failed split launch stops training until restored
         if (h->ds[0].rows == 0) throw FqErr{FQLPOP_E_STATE, "no training dataset set (fqlpop_set_dataset)"};
         HIPCHK(hipSetDevice(h->device));
         for (int i = 0; i < n_steps; ++i) {
@@ -2205,6 +2236,8 @@ int fqlpop_step_injected(fqlpop_t* h, const float* batch, const float* noise) {
     return guard([&] {
         ARGCHK(h && batch, "null argument");
         HIPCHK(hipSetDevice(h->device));
+        if (split_error_pending(h)) sync_all_streams(h);
+        check_split_error(h, -1, true);
         if (h->nz == 0) return;
         stage_injected(h, batch, noise);
         run(h, true, true, noise != nullptr);
@@ -2322,7 +2355,9 @@ static void state_copy(fqlpop* h, int member, int which, float* flat, const floa
     std::vector<float> blk((size_t)h->P), tblk((size_t)h->PT, 0.f);
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipDeviceSynchronize());
-    check_split_error(h);  // never export (checkpoint, member copy) parameters a failed launch wrote
+    // never export (checkpoint, member copy) state a failed launch wrote; a write restores it
+    if (get) check_split_error(h, member);
+    else (void)absorb_split_error(h);
     HIPCHK(hipMemcpy(blk.data(), arena + (long long)member * h->P, sizeof(float) * h->P, hipMemcpyDeviceToHost));
     if (which == 0)
         HIPCHK(hipMemcpy(tblk.data(), h->target + (long long)member * h->PT, sizeof(float) * h->PT,
@@ -2352,6 +2387,7 @@ static void state_copy(fqlpop* h, int member, int which, float* flat, const floa
             mirror_params(h, member, h->sM);
             HIPCHK(hipStreamSynchronize(h->sM));
         }
+        note_restored(h, member, which);
     }
 }
 
@@ -2377,7 +2413,7 @@ int fqlpop_get_count(fqlpop_t* h, int member, int32_t* count) {
         ARGCHK(count, "null argument");
         HIPCHK(hipSetDevice(h->device));
         HIPCHK(hipDeviceSynchronize());
-        check_split_error(h);
+        check_split_error(h, member);
         HIPCHK(hipMemcpy(count, h->count + member, sizeof(int), hipMemcpyDeviceToHost));
     });
 }
@@ -2402,7 +2438,11 @@ int fqlpop_set_member(fqlpop_t* h, int member, float alpha, uint64_t seed, int r
         HIPCHK(hipMemcpy(h->alpha + member, &alpha, sizeof(float), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(h->seeds + member, &seed, sizeof(uint64_t), hipMemcpyHostToDevice));
         upload_skey(h, member);
-        if (reinit) init_member(h, member, seed);
+        if (reinit) {
+            (void)absorb_split_error(h);
+            init_member(h, member, seed);
+            h->poisoned[member] = 0;  // a fresh member: nothing a failed launch wrote is left
+        }
     });
 }
 
@@ -2430,7 +2470,18 @@ int fqlpop_sync(fqlpop_t* h) {
         ARGCHK(h, "null handle");
         HIPCHK(hipSetDevice(h->device));
         sync_all_streams(h);
-        check_split_error(h);
+        // reported once here; the members stay poisoned for step / get_state / get_count / read_info
+        if (absorb_split_error(h)) throw FqErr{FQLPOP_E_STATE, kSplitFailMsg};
+    });
+}
+
+int fqlpop_debug_fail_split(fqlpop_t* h) {
+    return guard([&] {
+        ARGCHK(h, "null handle");
+        HIPCHK(hipSetDevice(h->device));
+        if (!h->split_err_host) throw FqErr{FQLPOP_E_STATE, "this population runs no split launch"};
+        sync_all_streams(h);
+        __atomic_store_n(h->split_err_host, 1u, __ATOMIC_RELEASE);
     });
 }
 

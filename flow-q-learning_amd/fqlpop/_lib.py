@@ -114,6 +114,7 @@ _SIGS = {
                                         ctypes.POINTER(ctypes.c_int),
                                         ctypes.POINTER(ctypes.c_int64)]),
     "fqlpop_sync": (ctypes.c_int, [_P]),
+    "fqlpop_debug_fail_split": (ctypes.c_int, [_P]),
     "fqlpop_time_dominant_kernel": (ctypes.c_int, [_P, ctypes.c_int,
                                                    ctypes.POINTER(ctypes.c_double),
                                                    ctypes.POINTER(ctypes.c_double)]),

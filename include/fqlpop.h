@@ -200,8 +200,18 @@ int fqlpop_num_leaves(fqlpop_t* h, int* n);
 int fqlpop_leaf_info(fqlpop_t* h, int i, char* name, int name_cap, int64_t* offset,
                      int* ndim, int64_t* shape3);
 
-/* Waits for all work of the handle. */
+/* Waits for all work of the handle.  Reports (once) a split launch that gave up; the
+ * members it stepped stay poisoned: fqlpop_step / _step_injected refuse while an active
+ * member is poisoned, fqlpop_get_state / _get_count refuse for a poisoned member and
+ * fqlpop_read_info while any is, until fqlpop_set_state has restored the member's params,
+ * Adam m and Adam v (or fqlpop_set_member reinit).  [EXT: a JAX error surfaces at the next
+ * blocking call of the reference's jitted update] */
 int fqlpop_sync(fqlpop_t* h);
+/* Test hook: sets the handle's split-error word exactly as a split launch whose hand-off
+ * wait gave up does (kernels.hip sp_fail), so the error path above can be exercised without
+ * a fault.  FQLPOP_E_STATE if the population runs no split launch.  [no reference
+ * counterpart] */
+int fqlpop_debug_fail_split(fqlpop_t* h);
 
 /* Measurement hook for bench.py: replays the dominant kernel (the hidden-
  * layer forward GEMM of the Euler flow, all active members in one launch)

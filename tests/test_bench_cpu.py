@@ -156,16 +156,21 @@ def _bench_module():
 
 
 def test_cpu_allotment_takes_the_smallest_bound(monkeypatch):
-    """The CPU leg's thread count is min(sched_getaffinity, cgroup quota, OMP_NUM_THREADS):
-    the GPU box's affinity mask shows 256 CPUs while the job's share is 16."""
+    """The CPU leg's thread count is min(sched_getaffinity, cgroup quota): the GPU box's
+    affinity mask shows 256 CPUs while the job's share is 16.  OMP_NUM_THREADS
+    is recorded but is not a cap (OMP_NUM_THREADS=1 from a launcher must not make
+    the baseline single-threaded)."""
     b = _bench_module()
-    monkeypatch.setenv("OMP_NUM_THREADS", "3")
-    assert b.cpu_allotment()["effective_cpus"] == min(3, len(os.sched_getaffinity(0)))
+    ncpu = len(os.sched_getaffinity(0))
+    monkeypatch.setattr(b, "_cgroup_cpu_quota", lambda: None)
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    got = b.cpu_allotment()
+    assert got["effective_cpus"] == ncpu and got["omp_num_threads"] == "1"
     monkeypatch.setattr(b, "_cgroup_cpu_quota", lambda: 2)
-    assert b.cpu_allotment()["effective_cpus"] == min(2, len(os.sched_getaffinity(0)))
+    assert b.cpu_allotment()["effective_cpus"] == min(2, ncpu)
     monkeypatch.delenv("OMP_NUM_THREADS")
     monkeypatch.setattr(b, "_cgroup_cpu_quota", lambda: None)
-    assert b.cpu_allotment()["effective_cpus"] == len(os.sched_getaffinity(0))
+    assert b.cpu_allotment()["effective_cpus"] == ncpu
 
 
 def test_cpu_baseline_is_bounded_when_oversubscribed():

@@ -153,3 +153,52 @@ def test_prune_and_revive_split_bit_identical():
     assert np.array_equal(got[2], ref[2])
     for i, (x, y) in enumerate(zip(got[0], ref[0])):
         assert np.array_equal(x, y), f"state {i} differs"
+
+
+def test_split_euler_pre0_non_tail_shape_bit_identical():
+    """the split Euler flow's layer-0 precompute (PRE0) for a shape WITHOUT the
+    layer-0 tail k-step: obs 24, act 4 (K0 = 29: 8 k-steps, 6 of them observation rows, 2 of
+    the step's own) against the unsplit kernel, 1 and 2 members."""
+    for n in (1, 2):
+        ref = _run({"split": 0}, n, D=24, A=4)
+        got = _run({}, n, D=24, A=4)
+        assert got[3].startswith("split_fwd_kernel"), got[3]
+        _same(got, ref)
+
+
+def test_split_failure_is_sticky_until_restored():
+    """a split launch that gave up poisons the members it stepped.  The
+    error is reported by the next call, and then step, get_state, get_count and read_info keep
+    refusing a poisoned member (no checkpoint of state such a launch wrote) until its params,
+    Adam m and Adam v are restored with set_state; the restored member exports again and the
+    population trains again once every member is restored."""
+    from fqlpop import FqlpopError, Population, PopulationConfig
+    from fqlpop._lib import check
+    pop = Population(PopulationConfig(hidden_dims=(512,) * 4, batch_size=256), [3.0, 30.0], [1, 2])
+    pop.set_dataset(_data(20_000, 28, 5, 4))
+    pop.step(2)
+    pop.sync()
+    saved = [[pop.get_flat(i, w) for w in (0, 1, 2)] for i in range(2)]
+    count = [pop.get_count(i) for i in range(2)]
+    check(pop.lib.fqlpop_debug_fail_split(pop._h))
+    with pytest.raises(FqlpopError, match="hand-off wait timed out"):
+        pop.step(1)
+    for call in (lambda: pop.step(1), lambda: pop.get_flat(0, 0), lambda: pop.get_flat(1, 1),
+                 lambda: pop.get_count(0), lambda: pop.read_info_array()):
+        with pytest.raises(FqlpopError, match="restore"):
+            call()
+    pop.sync()  # reported once; the poison stays
+    for w in (0, 1):  # params and m only: still poisoned
+        pop.set_flat(0, saved[0][w], w)
+    with pytest.raises(FqlpopError, match="member 0"):
+        pop.get_flat(0, 0)
+    pop.set_flat(0, saved[0][2], 2)
+    assert np.array_equal(pop.get_flat(0, 0), saved[0][0])
+    assert pop.get_count(0) == count[0]
+    with pytest.raises(FqlpopError, match="member 1"):
+        pop.step(1)
+    pop.set_member(1, 30.0, 2, reinit=True)
+    pop.step(2)
+    pop.sync()
+    assert np.all(np.isfinite(pop.read_info_array()[:, :13]))
+    pop.close()
