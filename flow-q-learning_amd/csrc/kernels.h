@@ -440,5 +440,7 @@ void launch_rollout(const RolloutArgs& a, hipStream_t s);
 // The C ABI's thread-local last-error message (runtime.cpp), for entry points
 // defined in other translation units (emtrain.hip).
 void set_last_error(const char* msg);
+// engine option em_seq_sweep (runtime.cpp), read by fqlpop_emtrain_create
+int engine_option_em_seq_sweep();
 
 }  // namespace fq

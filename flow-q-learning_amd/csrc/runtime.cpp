@@ -85,6 +85,8 @@ struct EngineOptions {
     int hw_queues = 4;     // the HIP runtime's hardware queues per process (GPU_MAX_HW_QUEUES, which the
                            // caller sets; the Python layer passes it): below 4 the step is captured on
                            // one stream (graph launch and hardware queues)
+    int em_seq_sweep = 1;  // env-model multistep training: the 1024-thread BPTT sweep with dW as a separate
+                           // GEMM (emtrain.hip); 0 = the round-5 kernel (dW inside the time loop)
 };
 // (Schedule experiments that measured slower were removed in round 4 and stay in git history
 // and DESIGN.md section 5: a 4th stream, stream priorities, the critic optimiser on the main
@@ -120,6 +122,7 @@ const EngineOptionRef kEngineOptions[] = {
     {"hw_queues", &EngineOptions::hw_queues, 1, 1024},
     {"split_sites", &EngineOptions::split_sites, 0, (1 << 24) - 1},
     {"split_blocks", &EngineOptions::split_blocks, 64, 1024},
+    {"em_seq_sweep", &EngineOptions::em_seq_sweep, 0, 1},
 };
 
 // ---------------------------------------------------------------- host Philox
@@ -1798,6 +1801,7 @@ void check_member(fqlpop* h, int member) {
 }  // namespace
 
 void fq::set_last_error(const char* msg) { g_err = msg ? msg : ""; }
+int fq::engine_option_em_seq_sweep() { return g_engine_opts.em_seq_sweep; }
 
 // =================================================================== C ABI ==
 extern "C" {

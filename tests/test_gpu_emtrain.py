@@ -298,3 +298,39 @@ def test_multistep_device_sampling_learns_and_driver(tmp_path):
     tree = em.load_flax_msgpack(out / "multistep.pt")["params"]
     cell = tree["ScanCell_0"]["cell"]
     assert cell["Dense_0"]["kernel"].shape == (D + A, 128) and cell["LayerNorm_0"]["scale"].shape == (D + A,)
+
+
+@pytest.mark.parametrize("tw,T", [(0.0, 48), (1.0, 16)])
+def test_multistep_sweep_matches_round5_kernel(tw, T):
+    """Round 6's multistep path (engine option em_seq_sweep: the 1024-thread BPTT sweep with
+    the next op's weight fragments in flight, dW as a GEMM over the stored records) against
+    round 5's em_seq_grad_kernel on the same device-sampled windows, one train step: logs
+    within 1e-4, Adam moments within 1e-3 of each leaf's scale and parameters as against the
+    oracle (only the order of the fp32 sums differs).  One step: an untrained cell rolled over
+    T steps diverges, so later steps amplify rounding differences (4 steps at T = 48 differed by
+    6.5e-4 in the loss).  Both paths are oracle-checked on injected batches above."""
+    from _helpers import engine_options
+    from envmodel.trainer import unflatten
+    D, A = 28, 5
+    ds = _trajectory_dataset(8, D, A, seed=5)
+    spec = em.EnvModelSpec(D, A, (128, 256, 128), (128, 256, 128))
+    sp = em.init_state_predictor(spec, 0)
+    tp = em.init_termination_predictor(spec, 2)
+    cfg = EnvModelTrainerConfig(steps=50, model="multistep", sequence_length=T, termination_weight=tw,
+                                batch_size=64, seed=9, init_learning_rate=1e-3)
+    out = {}
+    for path in (0, 1):
+        with engine_options(em_seq_sweep=path):
+            tr = StatePredictorTrainer(spec, sp, _Loader(ds), None, cfg, tp_params=tp if tw > 0 else None)
+            tr.steps(1)
+            out[path] = (tr.read_logs(), unflatten(tr._names, tr._shapes, tr.flat(0)),
+                         unflatten(tr._names, tr._shapes, tr.flat(1)))
+            tr.close()
+    for k, v in out[0][0].items():
+        assert out[1][0][k] == pytest.approx(v, rel=1e-4, abs=1e-7), k
+    for m in out[0][2]:
+        for k in out[0][2][m]:
+            w = out[0][2][m][k]
+            np.testing.assert_allclose(out[1][2][m][k], w, rtol=1e-3, atol=1e-3 * float(np.abs(w).max()) + 1e-12,
+                                       err_msg=f"m {m}/{k}")
+    _assert_params_close(out[1][1], _f64(out[0][1]), 1)
