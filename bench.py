@@ -403,7 +403,10 @@ def envmodel_train_leg(wl: dict, data: dict, steps: int) -> dict:
         tr.close()
     out["note"] = ("B=256, hidden (128, 256, 128), Adam + cosine decay; two launches per train_step "
                    "(fused fwd/loss/bwd over 16-row blocks, partial-sum Adam); multistep: 256-step "
-                   "windows of 1000-row episodes, backpropagation through time in one launch")
+                   "windows of 1000-row episodes, termination_weight 0: backpropagation through time as "
+                   "a forward and a backward sweep in one 1024-thread launch per 16 sequences, dW as a "
+                   "GEMM over the stored records, then Adam (engine option em_seq_sweep; "
+                   "profiles/round6b/em_multistep_ab_grouped.txt has termination_weight 1 too)")
     return out
 
 
