@@ -90,6 +90,9 @@ const char* fqlpop_last_error(void);
  *   with.  Below 4 the step is captured on one stream: ROCm 7's graph launch can index past
  *   its pool of branch streams when more than one shares the launch stream's hardware queue.
  *   A caller that sets GPU_MAX_HW_QUEUES passes it here (the Python Population does).
+ *   em_seq_sweep (0/1, default 1; read by fqlpop_emtrain_create): multistep env-model
+ *   training as a forward and a backward sweep per 16 sequences plus a dW GEMM (0: the
+ *   round-5 kernel with dW inside the time loop; same oracle tolerance).
  * The defaults are the measured-fastest configuration.  Unknown names or values
  * out of range: FQLPOP_E_ARG.  (Round 3's schedule experiments that measured slower --
  * streams, prio, cdw_sb, dw_stagger, xstep, bc_late, fuse_dq, early_join -- were
