@@ -673,8 +673,12 @@ __global__ __launch_bounds__(NT) void em_seq_grad_kernel(const StepArgs a) {
 // Taken when every op fits one unit per wave (fqlpop_emtrain_create: sw_fits); otherwise, and
 // under engine option em_seq_sweep = 0, em_seq_grad_kernel runs.
 constexpr int SW_NT = 1024, SW_NW = SW_NT / 64, SW_FM = 32, SW_SCR = SW_NW * 16 * R;
-constexpr int SW_RQ = 10;
-constexpr int EM_PH_N = 32;  // diagnostic phase slots (FQ_DIAG)  // a step's record, loaded a step ahead: <= SW_RQ floats per thread
+constexpr int SW_RQ = 10;    // a step's record, loaded a step ahead: <= SW_RQ floats per thread
+// diagnostic phase slots (FQ_DIAG, FQLPOP_EM_PROBE): 0 inputs, 26 LayerNorm statistics, 1
+// normalise, 2-5 forward ops, 6-13 termination-predictor ops, 27 record stores, 14 next
+// observation; backward: 28 record to LDS, 29 next record's loads, 15 barrier, 16 carry,
+// 17-20 dX ops, 30 LayerNorm backward sums, 25 carry update
+constexpr int EM_PH_N = 32;
 
 struct SwOp {
     const float* A;  // k-major [Kc][No] (No contiguous): W for a forward op, W^T for a dX op
@@ -997,6 +1001,7 @@ __global__ __launch_bounds__(SW_NT) void em_sweep_kernel(const StepArgs a) {
             rs_s[tid] = 1.0f / sqrtf(fmaxf(s2 / K0 - mu * mu, 0.f) + 1e-6f);
         }
         __syncthreads();
+        stamp(26);
         for (int q = tid; q < K0 * R; q += SW_NT) {
             const int k = q / R, r = q % R;
             const float xh = (x0[q] - mu_s[r]) * rs_s[r];
@@ -1064,6 +1069,7 @@ __global__ __launch_bounds__(SW_NT) void em_sweep_kernel(const StepArgs a) {
             float* sg = sa + act_floats;
             for (int q = tid; q < D * R; q += SW_NT) sg[q] = gA[q];
         }
+        stamp(27);
         const float* pred = tacts(0);
         for (int q = tid; q < D * R; q += SW_NT) x0[q] = pred[q];  // the next step's observation
         __syncthreads();
@@ -1112,7 +1118,9 @@ __global__ __launch_bounds__(SW_NT) void em_sweep_kernel(const StepArgs a) {
                 else if (q < n_rec) gA[q - n3] = rec[j];
             }
         }
+        stamp(28);
         rec_load(t - 1, tid);
+        stamp(29);
         __syncthreads();
         stamp(15);
         for (int q = tid; q < D * R; q += SW_NT) {
@@ -1158,6 +1166,7 @@ __global__ __launch_bounds__(SW_NT) void em_sweep_kernel(const StepArgs a) {
             cs[1][tid] = c2 / K0;
         }
         __syncthreads();
+        stamp(30);
         for (int q = tid; q < D * R; q += SW_NT) {
             const int k = q / R, r = q % R;
             carry[q] += rs_s[r] * (g[q] * lnp[k] - cs[0][r] - xhat[q] * cs[1][r]);
