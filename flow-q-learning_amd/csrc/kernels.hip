@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <type_traits>
+
 // The explicit waits (__builtin_amdgcn_s_waitcnt with vmcnt / lgkmcnt immediates, e.g. 0x0F74)
 // use the gfx9 simm16 field layout, which gfx10+ encodes differently; the v_permlane*_swap
 // inline asm exists on gfx950 only.  Device code is built for gfx950 alone (Makefile ARCH).
@@ -384,10 +386,40 @@ DEV void bstore4_aux(rsrc_t r, float4 v, int off_b, int nt) {
     else __builtin_amdgcn_raw_buffer_store_b128(w, r, off_b, 0, 0);
 }
 
-template <int BM, int BN, bool DUAL>
+// The epilogue's first batch of p, m, v (and target) rows, issued by the k-loop's last slice
+// (their loads do not depend on the gradient): their latency then runs under the last
+// slice's MFMAs and the gradient tile's staging instead of after it.  Same loads, same
+// registers' contents as the epilogue's own issue: bit-identical.
+constexpr int ADAM_U = 2;
+struct AdamPre {
+    float4 p[ADAM_U], m[ADAM_U], v[ADAM_U], t[ADAM_U];
+};
+template <int BM, int BN>
+DEV void adam_issue0(const AdamEpi& e, int gi, const GemmArgs& g, int slot, int y, int i0, int j0, AdamPre& pre) {
+    constexpr int TPR = BN / 4, RPI = 256 / TPR;
+    const int gM = uni(g.M), ldc = uni(g.ldc), tid = threadIdx.x;
+    const long long pb = uni64((long long)slot * e.P + e.w_off[gi] + (long long)y * e.ens);
+    const long long nleaf = (long long)gM * ldc;
+    const rsrc_t rP = make_rsrc(e.p_in + pb, nleaf);
+    const rsrc_t rM = make_rsrc(e.m + pb, nleaf), rV = make_rsrc(e.v + pb, nleaf);
+    const bool hasT = e.target != nullptr;
+    const rsrc_t rT = make_rsrc(uniptr(hasT ? e.target + (long long)slot * e.PT + e.w_off[gi] + (long long)y * e.ens
+                                            : e.m + pb), nleaf);
+    const int cj = (tid % TPR) * 4, ri = tid / TPR;
+#pragma unroll
+    for (int u = 0; u < ADAM_U; ++u) {
+        const int off = ((i0 + u * RPI + ri) * ldc + j0 + cj) * 4;
+        pre.p[u] = bload4_aux(rP, off, 0);
+        pre.m[u] = bload4_aux(rM, off, 1);
+        pre.v[u] = bload4_aux(rV, off, 1);
+        pre.t[u] = hasT ? bload4_aux(rT, off, 1) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+
+template <int BM, int BN, bool DUAL, bool PRE>
 DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc)[BM / 64][BN / 64],
                        f32x16 (&acc2)[BM / 64][BN / 64], int slot, int y, int tile, int per, int i0, int j0,
-                       int wi, int wj, int l32, int lh, float* smem) {
+                       int wi, int wj, int l32, int lh, float* smem, const AdamPre& pre) {
     constexpr int TM = BM / 64, TN = BN / 64;
     constexpr int PT = BN + 1;  // LDS row pitch (odd: the transposed read of pass 2 spreads over banks)
     // (the launching kernel sizes smem for the gradient tile: group_smem_floats)
@@ -413,7 +445,7 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
     // pass 1: thread -> 4 consecutive columns of a row, U rows per batch, two batches in
     // flight (p, m, v, target do not depend on the gradient: batch 0 is issued before the
     // gradient tile is staged); m, v and the target stream non-temporally
-    constexpr int TPR = BN / 4, RPI = 256 / TPR, U = 2, NB = BM / (RPI * U);
+    constexpr int TPR = BN / 4, RPI = 256 / TPR, U = ADAM_U, NB = BM / (RPI * U);
     static_assert(NB * RPI * U == BM && NB >= 2, "");
     const int cj = (tid % TPR) * 4, ri = tid / TPR;
     float4 p4[2][U], m4[2][U], v4[2][U], t4[2][U];
@@ -428,7 +460,17 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
             t4[q][u] = hasT ? bload4_aux(rT, off, 1) : float4{0.f, 0.f, 0.f, 0.f};
         }
     };
-    if (run) issue(0, 0);
+    if (PRE) {  // batch 0 issued by the k-loop's last slice (adam_issue0)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            p4[0][u] = pre.p[u];
+            m4[0][u] = pre.m[u];
+            v4[0][u] = pre.v[u];
+            t4[0][u] = pre.t[u];
+        }
+    } else if (run) {
+        issue(0, 0);
+    }
     __syncthreads();  // every wave is done with the operand buffers
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -567,16 +609,27 @@ DEV void gemm_body(const GemmArgs& g, int w, float* smem, const AdamEpi* ae = nu
 #pragma unroll
     for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC, RP>(Bs0, p, rb[p]);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
+    // EPI_ADAM: the last slice is peeled; instead of the (unused) prefetch it issues the
+    // optimiser epilogue's first batch (adam_issue0).  (Issued one slice earlier, behind that
+    // slice's prefetch, it measured slower: 156.6 against 154.6 us serial.)
+    constexpr bool PEEL = EPI == EPI_ADAM;
+    AdamPre pre;
+    auto slice = [&](int kt, auto last_c, auto issue_c) {
+        constexpr bool LAST = decltype(last_c)::value, ISSUE = decltype(issue_c)::value;
         const float* Ac = (kt & 1) ? As1 : As0;
         const float* Bc = (kt & 1) ? Bs1 : Bs0;
-        // prefetch the next slice (the last iteration re-reads a valid slice:
-        // no branch, so the loads stay in flight across the MFMAs)
-        const int kn = (kt + 1 < nk ? kt + 1 : kt) * BK;
+        if constexpr (ISSUE) {
+            if (ae->mode != 1) adam_issue0<BM, BN>(*ae, gi, g, slot, y, i0, j0, pre);
+        }
+        if constexpr (!LAST) {
+            // prefetch the next slice (the last iteration re-reads a valid slice:
+            // no branch, so the loads stay in flight across the MFMAs)
+            const int kn = (kt + 1 < nk ? kt + 1 : kt) * BK;
 #pragma unroll
-        for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, ARC>(rA, lda, p, i0, kn);
+            for (int p = 0; p < A_LD; ++p) ra[p] = stage_load<BM, BK, ARC>(rA, lda, p, i0, kn);
 #pragma unroll
-        for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, BRC>(rB, ldb, p, j0, kn);
+            for (int p = 0; p < B_LD; ++p) rb[p] = stage_load<BN, BK, BRC>(rB, ldb, p, j0, kn);
+        }
         // keep the prefetch at the top of the iteration (hipcc otherwise sinks
         // it next to its ds_write and exposes the whole global latency)
         __builtin_amdgcn_sched_barrier(0);
@@ -622,19 +675,27 @@ DEV void gemm_body(const GemmArgs& g, int w, float* smem, const AdamEpi* ae = nu
                     else
                         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk][a], bv[kk][b], acc[a][b], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        float* An = (kt & 1) ? As0 : As1;
-        float* Bn = (kt & 1) ? Bs0 : Bs1;
+        if constexpr (!LAST) {
+            float* An = (kt & 1) ? As0 : As1;
+            float* Bn = (kt & 1) ? Bs0 : Bs1;
 #pragma unroll
-        for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, ARC, RP>(An, p, ra[p]);
+            for (int p = 0; p < A_LD; ++p) stage_store<BM, BK, ARC, RP>(An, p, ra[p]);
 #pragma unroll
-        for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC, RP>(Bn, p, rb[p]);
-        __syncthreads();
+            for (int p = 0; p < B_LD; ++p) stage_store<BN, BK, BRC, RP>(Bn, p, rb[p]);
+            __syncthreads();
+        }
+    };
+    if constexpr (PEEL) {
+        for (int kt = 0; kt < nk - 1; ++kt) slice(kt, std::false_type{}, std::false_type{});
+        slice(nk - 1, std::true_type{}, std::true_type{});
+    } else {
+        for (int kt = 0; kt < nk; ++kt) slice(kt, std::false_type{}, std::false_type{});
     }
 
     // epilogue: accumulator register r of a 32x32 tile holds
     // row i = (r&3) + 8*(r>>2) + 4*(lane>>5), column j = lane&31.
     if constexpr (EPI == EPI_ADAM) {
-        adam_epilogue<BM, BN, DUAL>(*ae, gi, g, acc, acc2, slot, y, tile, per, i0, j0, wi, wj, l32, lh, smem);
+        adam_epilogue<BM, BN, DUAL, true>(*ae, gi, g, acc, acc2, slot, y, tile, per, i0, j0, wi, wj, l32, lh, smem, pre);
         return;
     }
     float* __restrict__ C = at(g.C, slot, y);
