@@ -129,6 +129,30 @@ DEV float block_min(float v, float* red) {
     return fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
 }
 
+// N block-wide reductions in ONE pair of barriers: the same wave reductions and the same
+// cross-wave order as N successive block_sum / block_max / block_min calls, so the results
+// are bit-identical to those (which take two barriers each).  kind[i]: 0 sum, 1 max, 2 min;
+// red: 8 N floats (up to 8 waves write; waves 0..3 are combined, as above).
+template <int N>
+DEV void block_reduce_n(float (&v)[N], const int (&kind)[N], float* red) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = kind[i] == 1 ? wave_max(v[i]) : kind[i] == 2 ? wave_min(v[i]) : wave_sum(v[i]);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) red[i * 8 + w] = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const float* r = red + i * 8;
+        v[i] = kind[i] == 1   ? fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3]))
+               : kind[i] == 2 ? fminf(fminf(r[0], r[1]), fminf(r[2], r[3]))
+                              : r[0] + r[1] + r[2] + r[3];
+    }
+}
+
 // Block-uniform values through readfirstlane (SGPRs): see gemm_body
 DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 DEV long long uni64(long long v) {
@@ -236,10 +260,12 @@ DEV void adam_chunk_t(const AdamArgs& a, int bx, int z) {
             }
         }
     }
-    __shared__ float red[NT / 64];
-    mx = block_max(mx, red);
-    mn = block_min(mn, red);
-    ss = block_sum(ss, red);
+    __shared__ float red[3 * 8];
+    float st3[3] = {mx, mn, ss};
+    block_reduce_n<3>(st3, {1, 2, 0}, red);
+    mx = st3[0];
+    mn = st3[1];
+    ss = st3[2];
     if (threadIdx.x == 0) {
         float* st = a.stats + ((long long)slot * a.n_total_chunks + ci) * 3;
         st[0] = mx;
@@ -517,10 +543,12 @@ DEV void adam_epilogue(const AdamEpi& e, int gi, const GemmArgs& g, f32x16 (&acc
             }
         }
     }
-    __shared__ float red[4];
-    mx = block_max(mx, red);  // (its barriers also publish the new p in LDS)
-    mn = block_min(mn, red);
-    ss = block_sum(ss, red);
+    __shared__ float red[3 * 8];
+    float st3[3] = {mx, mn, ss};
+    block_reduce_n<3>(st3, {1, 2, 0}, red);  // (its barriers also publish the new p in LDS)
+    mx = st3[0];
+    mn = st3[1];
+    ss = st3[2];
     if (tid == 0) {
         float* st = e.stats + ((long long)slot * e.n_total_chunks + e.stat_base[gi] + y * per + tile) * 3;
         st[0] = mx;
@@ -3546,7 +3574,7 @@ void launch_sample(const SampleArgs& a, hipStream_t s) {
 __global__ __launch_bounds__(256) void loss_critic_kernel(const LossArgs a) {
     const int z = blockIdx.x, slot = a.slots[z];
     const int B = a.B, E = a.E, A = a.A;
-    __shared__ float red[4];
+    __shared__ float red[11 * 8];
     const float* q = at(a.q, slot);      // [E][2B] (ens stride = q.sy)
     const float* qt = at(a.qt, slot);    // [E][B]
     const float* rw = at(a.rew, slot);
@@ -3588,17 +3616,17 @@ __global__ __launch_bounds__(256) void loss_critic_kernel(const LossArgs a) {
         const float d = am[i] - ac[i];
         smse += d * d;
     }
-    sq = block_sum(sq, red);
-    qs = block_sum(qs, red);
-    qmx = block_max(qmx, red);
-    qmn = block_min(qmn, red);
-    qpi_s = block_sum(qpi_s, red);
-    qpi_abs = block_sum(qpi_abs, red);
-    smse = block_sum(smse, red);
-    for (int e = 0; e < E && e < 4; ++e) {
-        const float s = block_sum(sdq[e], red);
-        if (threadIdx.x == 0) at(a.g_cb4, slot, e)[0] = s;
-    }
+    float rv[11] = {sq, qs, qmx, qmn, qpi_s, qpi_abs, smse, sdq[0], sdq[1], sdq[2], sdq[3]};
+    block_reduce_n<11>(rv, {0, 0, 1, 2, 0, 0, 0, 0, 0, 0, 0}, red);
+    sq = rv[0];
+    qs = rv[1];
+    qmx = rv[2];
+    qmn = rv[3];
+    qpi_s = rv[4];
+    qpi_abs = rv[5];
+    smse = rv[6];
+    if (threadIdx.x == 0)
+        for (int e = 0; e < E && e < 4; ++e) at(a.g_cb4, slot, e)[0] = rv[7 + e];
     const float qmean_pi = qpi_s / (float)B;
     const float lam = a.normq ? 1.0f / (qpi_abs / (float)B) : 1.0f;
     const float gpi = -lam * invEB;
@@ -3620,7 +3648,7 @@ __global__ __launch_bounds__(256) void loss_critic_kernel(const LossArgs a) {
 __global__ __launch_bounds__(256) void loss_bc_kernel(const LossArgs a) {
     const int z = blockIdx.x, slot = a.slots[z];
     const int B = a.B, A = a.A;
-    __shared__ float red[4];
+    __shared__ float red[9 * 8];
     const float* vp = at(a.vpred, slot);
     const float* ac = at(a.act, slot);
     const float* x0 = at(a.x0, slot);
@@ -3643,11 +3671,11 @@ __global__ __launch_bounds__(256) void loss_bc_kernel(const LossArgs a) {
             }
         }
     }
-    s = block_sum(s, red);
-    for (int j = 0; j < A; ++j) {
-        const float t = block_sum(sdb[j], red);
-        if (threadIdx.x == 0) at(a.g_bcb4, slot)[j] = t;
-    }
+    float rv[9] = {s, sdb[0], sdb[1], sdb[2], sdb[3], sdb[4], sdb[5], sdb[6], sdb[7]};
+    block_reduce_n<9>(rv, {0, 0, 0, 0, 0, 0, 0, 0, 0}, red);
+    s = rv[0];
+    if (threadIdx.x == 0)
+        for (int j = 0; j < A; ++j) at(a.g_bcb4, slot)[j] = rv[1 + j];
     if (threadIdx.x == 0) at(a.info, slot)[5] = s / (float)(A * B);
 }
 
@@ -3657,7 +3685,7 @@ __global__ __launch_bounds__(256) void loss_bc_kernel(const LossArgs a) {
 __global__ __launch_bounds__(256) void loss_actor_kernel(const LossArgs a) {
     const int z = blockIdx.x, slot = a.slots[z];
     const int B = a.B, A = a.A;
-    __shared__ float red[4];
+    __shared__ float red[9 * 8];
     const float alpha = a.alpha[slot];
     const float* ap = at(a.apiraw, slot);
     const float* af = at(a.aflow, slot);
@@ -3686,11 +3714,11 @@ __global__ __launch_bounds__(256) void loss_actor_kernel(const LossArgs a) {
             }
         }
     }
-    s = block_sum(s, red);
-    for (int j = 0; j < A; ++j) {
-        const float t = block_sum(sdb[j], red);
-        if (threadIdx.x == 0) at(a.g_osb4, slot)[j] = t;
-    }
+    float rv[9] = {s, sdb[0], sdb[1], sdb[2], sdb[3], sdb[4], sdb[5], sdb[6], sdb[7]};
+    block_reduce_n<9>(rv, {0, 0, 0, 0, 0, 0, 0, 0, 0}, red);
+    s = rv[0];
+    if (threadIdx.x == 0)
+        for (int j = 0; j < A; ++j) at(a.g_osb4, slot)[j] = rv[1 + j];
     if (threadIdx.x == 0) {
         float* info = at(a.info, slot);
         const float distill = s / (float)(A * B);
