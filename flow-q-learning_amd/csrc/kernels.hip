@@ -101,38 +101,12 @@ DEV float lk_sum(float v) {
     return s + c;
 }
 
-// Block-wide reductions over the first 4 waves (256 threads); `red` needs one float per
-// wave.  In a 512-thread block the other waves only join the barriers (their values are
-// ignored), so the result is the 256-thread one, bit for bit.
-DEV float block_sum(float v, float* red) {
-    v = wave_sum(v);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    return red[0] + red[1] + red[2] + red[3];
-}
-DEV float block_max(float v, float* red) {
-    v = wave_max(v);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-}
-DEV float block_min(float v, float* red) {
-    v = wave_min(v);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    return fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
-}
-
-// N block-wide reductions in ONE pair of barriers: the same wave reductions and the same
-// cross-wave order as N successive block_sum / block_max / block_min calls, so the results
-// are bit-identical to those (which take two barriers each).  kind[i]: 0 sum, 1 max, 2 min;
-// red: 8 N floats (up to 8 waves write; waves 0..3 are combined, as above).
+// N block-wide reductions over the first 4 waves (256 threads) in ONE pair of barriers:
+// each value's wave reduction (butterfly), then the 4 wave results combined left to right
+// (red[0] + red[1] + red[2] + red[3]; max / min pairwise), the order of the round-5
+// one-value-per-barrier-pair reductions, so the results are bit-identical to those.
+// kind[i]: 0 sum, 1 max, 2 min; red: 8 N floats.  In a 512-thread block the other waves
+// only join the barriers (their values are ignored), so the result is the 256-thread one.
 template <int N>
 DEV void block_reduce_n(float (&v)[N], const int (&kind)[N], float* red) {
 #pragma unroll
