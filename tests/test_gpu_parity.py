@@ -360,13 +360,17 @@ def _synthetic_rows(N, D, A, seed):
 _C2_ALPHAS = np.logspace(np.log10(3), np.log10(1000), 16).tolist()   # bench.py / tune_alpha.py:43-45
 
 
-@pytest.mark.parametrize("D,A,B,alphas,steps,kw", [
-    (28, 5, 256, [10.0, 216.8], 3, {}),               # C2 shapes, 2 members: the split launches (auto)
-    (28, 5, 256, _C2_ALPHAS, 2, {}),                  # BASELINE C2: the benchmarked 16-member population
-    (42, 8, 1024, [31.6], 3, dict(discount=0.995)),   # BASELINE C3 shapes (antsoccer)
-    (42, 8, 1024, _C2_ALPHAS[::4], 2, dict(discount=0.995)),  # C3, 4 members
+@pytest.mark.parametrize("D,A,B,alphas,steps,kw,check", [
+    (28, 5, 256, [10.0, 216.8], 3, {}, None),               # C2 shapes, 2 members: the split launches (auto)
+    (28, 5, 256, _C2_ALPHAS, 2, {}, None),                  # BASELINE C2: the benchmarked 16-member population
+    (42, 8, 1024, [31.6], 3, dict(discount=0.995), None),   # BASELINE C3 shapes (antsoccer)
+    (42, 8, 1024, _C2_ALPHAS[::4], 2, dict(discount=0.995), None),  # C3, 4 members
+    # BASELINE C3 itself: the full 16-member antsoccer population at B = 1024 steps on the
+    # device; every other member (slots 0, 2, ..., 14) is oracle-checked (2.5-6 s of float64
+    # oracle per member-step: all 16 would keep the test silent for up to 1.5 minutes)
+    (42, 8, 1024, _C2_ALPHAS, 1, dict(discount=0.995), list(range(0, 16, 2))),
 ])
-def test_production_step_matches_oracle_on_its_own_draws(D, A, B, alphas, steps, kw):
+def test_production_step_matches_oracle_on_its_own_draws(D, A, B, alphas, steps, kw, check):
     """fqlpop_step -- the path Trainer and bench.py run -- against the oracle: the device
     sampler's rows, flow times and noises are reproduced on the host (tests/philox_np.py,
     Philox4x32-10 pinned to the Random123 known answers), the oracle updates on
@@ -388,13 +392,14 @@ def test_production_step_matches_oracle_on_its_own_draws(D, A, B, alphas, steps,
         pop.set_params(i, O.cast_tree(p, np.float32))
     keys = [sample_key(int(pop.seeds[i]), float(pop.alphas[i])) for i in range(len(alphas))]
     d64 = O.cast_tree(data, np.float64)
-    checks = [OptimiserChecker(pop, i, ocfgs[i].lr, ocfgs[i].tau) for i in range(len(alphas))]
+    members = list(range(len(alphas))) if check is None else check
+    checks = {i: OptimiserChecker(pop, i, ocfgs[i].lr, ocfgs[i].tau) for i in members}
     for step in range(steps):
-        for c in checks:
+        for c in checks.values():
             c.before()
         pop.step(1)
         info = pop.read_info("train")
-        for i in range(len(alphas)):
+        for i in members:
             idx, noise = draw(keys[i], step, B, N, A)
             batch = {k: v[idx] for k, v in d64.items()}
             params[i], opts[i], oinfo = O.update(ocfgs[i], params[i], opts[i], batch, noise)
