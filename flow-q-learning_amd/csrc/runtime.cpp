@@ -913,7 +913,7 @@ void stream_bwd_net(const Ctx& c, hipStream_t s, const NetLayout& N, TRef dout, 
     r.w5_off = N.W[N.L];
     r.L = N.L; r.H = N.H; r.ln = N.ln ? 1 : 0;
     r.ny = N.E; r.nz = c.nz; r.slots = h->slots;
-    launch_colsum_reduce(r, sw);
+    if (!(skip_mask() & 512)) launch_colsum_reduce(r, sw);
     // dW_l = X_l^T du_l over the first Mg columns, every layer in one grouped launch
     auto act = [&](float* p) { return tref(p + coff, act_ss, act_sy); };
     std::vector<GemmArgs> gs;
@@ -1121,7 +1121,8 @@ void launch_euler(fqlpop* h, const EulerArgs& ea, hipStream_t s) {
 // FQLPOP_SKIP (diagnostic builds only; TIMING EXPERIMENT, results are garbage): bit mask
 // of launches left out of the step, to measure each one's marginal cost in the concurrent
 // step: 1 Euler flow, 2 target-critic fwd, 4 critic fwd, 8 one-step fwd, 16 BC fwd,
-// 32 critic bwd (dX chain), 64 BC bwd, 128 one-step bwd.  Always 0 in the production build.
+// 32 critic bwd (dX chain), 64 BC bwd, 128 one-step bwd, 256 actor loss, 512 the three
+// colsum reductions.  Always 0 in the production build.
 int skip_mask() {
     static const int m = [] { const char* v = diag_env("FQLPOP_SKIP"); return v ? std::atoi(v) : 0; }();
     return m;
@@ -1567,7 +1568,7 @@ void enqueue(fqlpop* h, bool train, bool inj_batch, bool inj_noise) {
     }
     if (sF != sM) HIPCHK(hipStreamWaitEvent(sM, h->ev_flow, 0));
     if (sB != sM) HIPCHK(hipStreamWaitEvent(sM, h->ev_bcloss, 0));
-    launch_loss_actor(la, sM);
+    if (!(skip_mask() & 256)) launch_loss_actor(la, sM);
     if (train) {
         const NetLayout& N = h->os;
         if (h->fused_adam) {
